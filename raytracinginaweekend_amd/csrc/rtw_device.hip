@@ -1,0 +1,1299 @@
+// rtw_device.hip -- the MI355X (gfx950) path-tracing megakernel and its C ABI.
+//
+// Hot path restated for the device (reference: src/lib/rendering.rs:19-220):
+//   one wave = 64 pixels of one image tile; one lane = one pixel, iterating its samples in
+//   order (so the per-pixel f32 sum is the reference's sequential `.sum::<Color>()`,
+//   rendering.rs:172-179); a finished path immediately regenerates the lane's next camera
+//   sample, so a wave keeps every lane busy until its pixels' sample budgets are spent.
+//   BVH traversal is iterative with a per-lane stack in LDS, visiting nodes in exactly the
+//   reference's recursive order (hittable.rs:429-462: per-axis slab test with the CURRENT
+//   t_range, near child first by ray.direction[axis] > 0, both children always visited).
+//   Candidate tests compute only `t`; the hit record (position / normal / uv / front_face) is
+//   rebuilt once for the closest leaf -- a pure function of (leaf, ray, t), so it equals the
+//   record the reference builds eagerly.  Volumes draw their RNG during traversal in the same
+//   order as the reference.
+//
+// Scene data lives in one HBM arena as SoA float4 streams (see DESIGN.md "Data layout").
+// Numerics: -ffp-contract=off, no fast-math; shared scalar spec in include/rtw_scalar.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rtw_scalar.h"
+#include "rtw_common.h"
+
+#define RTW_BLOCK 256
+#define RTW_WAVES_PER_BLOCK (RTW_BLOCK / 64)
+#define RTW_STACK 32
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// device data
+// ---------------------------------------------------------------------------------------------
+struct DWorld {
+    const float4* node_a;  // {min.x, min.y, min.z, max.x}
+    const float4* node_b;  // {max.y, max.z, bits(left << 2 | axis), bits(right)}
+    const int4* leaf_info; // {geom_kind, geom_index, material, flags}
+    const float4* leaf_xf; // 3 per leaf: {neg_inv_density, off.xyz}, {ys, yc, vel.x, vel.y}, {vel.z,0,0,0}
+    const float4* spheres; // {center.xyz, radius}
+    const float4* rects;   // 2 per rect: {dist, r0.0, r0.1, r1.0}, {r1.1, bits(plane), 0, 0}
+    const float4* boxes;   // 2 per box: {min.xyz, max.x}, {max.y, max.z, 0, 0}
+    const float4* tri_pos; // 3 per tri: {p0.xyz, p1.x}, {p1.yz, p2.xy}, {p2.z, 0, 0, 0}
+    const float4* tri_attr; // 4 per tri: normals and uvs packed
+    const int4* materials; // {kind, texture, bits(fuzz), bits(ior)}
+    const int4* textures;  // 3 per texture
+    const int4* images;    // {texel offset, width, height, 0}
+    const uint32_t* texels; // RGBA8, row 0 = top
+    const float* perlin_ranvec; // 768 floats per perlin
+    const uint32_t* perlin_perm; // 768 per perlin (x, y, z)
+    const int* perlin_bits;
+    const struct WorldConst* wc; // camera / light / background, read from memory when used
+    int32_t root;
+    int32_t has_light;
+};
+
+// Rarely-read scalars live in HBM (scalar-cache loads at their use sites) instead of kernel
+// arguments, so they do not pin SGPRs across the bounce loop.
+struct WorldConst {
+    rtw_camera cam;
+    rtw_rect light;
+    rtw_background bg;
+};
+
+struct KArgs {
+    DWorld w;
+    int32_t width, height;
+    uint32_t spp;
+    int32_t max_depth;
+    int32_t mode;
+    int32_t layout;
+    int32_t tile_w, tile_h, tiles_x, n_tiles;
+    int32_t part_index, part_count;
+    int32_t chunks_per_tile; // ceil(tile_w * tile_h / 64)
+    int64_t jobs;            // waves of work in this launch
+    uint64_t seed_key;
+    float sx, sy;            // 1/(W-1), 1/(H-1)
+    rtw_uniform ux, uy;      // pixel jitter distributions
+    float* out;
+    unsigned long long* stats; // 13 counters (stats variant only)
+};
+
+// ---------------------------------------------------------------------------------------------
+// f32 vector algebra (vec3.rs), evaluated exactly as written in the reference
+// ---------------------------------------------------------------------------------------------
+struct V3 {
+    float x, y, z;
+};
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 mul(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 divs(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ V3 conv(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float len(V3 a) { return __builtin_sqrtf(dot(a, a)); }
+__device__ __forceinline__ V3 unit(V3 a) { return mul(a, 1.0f / len(a)); }  // vec3.rs:205-210
+__device__ __forceinline__ float comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+__device__ __forceinline__ void setc(V3& a, int i, float v) {
+    if (i == 0) a.x = v;
+    else if (i == 1) a.y = v;
+    else a.z = v;
+}
+__device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
+__device__ __forceinline__ V3 reflect(V3 d, V3 n) { return sub(d, mul(n, 2.0f * dot(d, n))); }  // vec3.rs:232
+__device__ __forceinline__ V3 refract(V3 d, V3 n, float eta) {  // vec3.rs:235-240
+    const float cos_theta = rtw_minr(dot(neg(d), n), 1.0f);
+    const V3 perp = mul(add(d, mul(n, cos_theta)), eta);
+    const float k = -__builtin_sqrtf(__builtin_fabsf(1.0f - dot(perp, perp)));
+    return add(perp, mul(n, k));
+}
+
+#define F32_PI 3.14159274101257324219f
+#define F32_TAU 6.28318548202514648438f
+#define F32_INF (__builtin_inff())
+
+// Out-of-line wrappers: the f64 polynomial constants need SGPR pairs (no VOP3 literals on
+// gfx9); inlined into the bounce loop they get hoisted and pin ~100 SGPRs.
+__device__ __noinline__ float d_acosf(float x) { return rtw_acosf(x); }
+__device__ __noinline__ float d_atan2f(float y, float x) { return rtw_atan2f(y, x); }
+__device__ __noinline__ float d_logf(float x) { return rtw_logf(x); }
+__device__ __noinline__ float d_sinf(float x) { return rtw_sinf(x); }
+
+struct Ray {
+    V3 o, d;
+    float time;
+};
+__device__ __forceinline__ V3 at(const Ray& r, float t) { return add(r.o, mul(r.d, t)); }
+__device__ __forceinline__ bool contains(float s, float e, float t) { return s <= t && t < e; }
+
+// ---------------------------------------------------------------------------------------------
+// statistics (stats variant only)
+// ---------------------------------------------------------------------------------------------
+enum {
+    ST_SAMPLES, ST_RAYS, ST_NODES, ST_T_SPHERE, ST_T_RECT, ST_T_BOX, ST_T_TRI,
+    ST_H_SPHERE, ST_H_RECT, ST_H_BOX, ST_H_TRI, ST_MAT, ST_TEXEL, ST_COUNT
+};
+struct Stats {
+    uint32_t c[ST_COUNT];
+};
+
+// ---------------------------------------------------------------------------------------------
+// primitives: candidate tests return t only
+// ---------------------------------------------------------------------------------------------
+// sphere_geometry.rs:21-41
+__device__ __forceinline__ bool sphere_t(float4 s, const Ray& r, float ts, float te, float& t) {
+    const V3 oc = sub(r.o, v3(s.x, s.y, s.z));
+    const float half_b = dot(oc, r.d);
+    const float c = dot(oc, oc) - s.w * s.w;
+    const float disc = half_b * half_b - c;
+    if (disc < 0.0f) return false;
+    const float sq = __builtin_sqrtf(disc);
+    const float small = -half_b - sq;
+    if (contains(ts, te, small)) {
+        t = small;
+        return true;
+    }
+    const float large = -half_b + sq;
+    if (contains(ts, te, large)) {
+        t = large;
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ void rect_axes(int plane, int& p0, int& p1, int& n) {
+    p0 = (plane == RTW_PLANE_YZ) ? 1 : 0;
+    p1 = (plane == RTW_PLANE_XY) ? 1 : 2;
+    n = (plane == RTW_PLANE_XY) ? 2 : ((plane == RTW_PLANE_XZ) ? 1 : 0);
+}
+struct RectG {
+    int plane;
+    float dist, r00, r01, r10, r11;
+};
+__device__ __forceinline__ RectG load_rect(const DWorld& w, int i) {
+    const float4 a = w.rects[2 * i], b = w.rects[2 * i + 1];
+    return RectG{__float_as_int(b.y), a.x, a.y, a.z, a.w, b.x};
+}
+// rect_geometry.rs:33-46 (hit test part)
+__device__ __forceinline__ bool rect_t(const RectG& g, const Ray& r, float ts, float te, float& t, V3& pos) {
+    int p0, p1, n;
+    rect_axes(g.plane, p0, p1, n);
+    t = (g.dist - comp(r.o, n)) / comp(r.d, n);
+    if (!contains(ts, te, t)) return false;
+    pos = add(r.o, mul(r.d, t));
+    const float a = comp(pos, p0), b = comp(pos, p1);
+    return a >= g.r00 && a <= g.r01 && b >= g.r10 && b <= g.r11;
+}
+
+// aabb.rs:103-167
+__device__ __forceinline__ bool box_line(float4 ba, float4 bb, const Ray& r, float& nt, int& np, float& ft, int& fp) {
+    const V3 mn = sub(v3(ba.x, ba.y, ba.z), r.o);
+    const V3 mx = sub(v3(ba.w, bb.x, bb.y), r.o);
+    float near = -F32_INF, far = F32_INF;
+    np = 0;
+    fp = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float t1 = comp(mn, a) / comp(r.d, a);
+        const float t2 = comp(mx, a) / comp(r.d, a);
+        const float tmin = rtw_minr(t1, t2);
+        const float tmax = rtw_maxr(t1, t2);
+        if (tmin > near) {
+            near = tmin;
+            np = a;
+        }
+        if (tmax < far) {
+            far = tmax;
+            fp = a;
+        }
+        if (near > far || far < 0.0f) return false;
+    }
+    nt = near;
+    ft = far;
+    return true;
+}
+__device__ __forceinline__ bool box_t(const DWorld& w, int i, const Ray& r, float ts, float te, float& t) {
+    float nt, ft;
+    int np, fp;
+    if (!box_line(w.boxes[2 * i], w.boxes[2 * i + 1], r, nt, np, ft, fp)) return false;
+    if (contains(ts, te, nt)) {
+        t = nt;
+        return true;
+    }
+    if (contains(ts, te, ft)) {
+        t = ft;
+        return true;
+    }
+    return false;
+}
+
+struct TriP {
+    V3 p0, p1, p2;
+};
+__device__ __forceinline__ TriP load_tri(const DWorld& w, int i) {
+    const float4 a = w.tri_pos[3 * i], b = w.tri_pos[3 * i + 1], c = w.tri_pos[3 * i + 2];
+    return TriP{v3(a.x, a.y, a.z), v3(a.w, b.x, b.y), v3(b.z, b.w, c.x)};
+}
+// triangle_geometry.rs:13-45; returns barycentrics for the record pass
+__device__ __forceinline__ bool tri_test(const TriP& T, const Ray& r, float ts, float te, float& t, V3& pos,
+                                         float& w0, float& w1, float& w2) {
+    const V3 dir1 = sub(T.p1, T.p0);
+    const V3 dir2 = sub(T.p2, T.p0);
+    const V3 normal = unit(cross(dir1, dir2));
+    const float denom = dot(r.d, normal);
+    if (!(__builtin_fabsf(denom) > 0.0001f)) return false;
+    t = dot(sub(T.p0, r.o), normal) / denom;
+    if (!contains(ts, te, t)) return false;
+    pos = at(r, t);
+    const V3 q = sub(pos, T.p0);
+    V3 vt = cross(normal, dir2);
+    w1 = dot(q, vt) / dot(dir1, vt);
+    if (!(w1 > 0.0f && w1 < 1.0f)) return false;
+    vt = cross(normal, dir1);
+    w2 = dot(q, vt) / dot(dir2, vt);
+    w0 = 1.0f - w1 - w2;
+    return w2 > 0.0f && w0 > 0.0f;
+}
+
+template <bool STATS>
+__device__ __forceinline__ bool geom_t(const DWorld& w, int kind, int idx, const Ray& r, float ts, float te, float& t,
+                                       Stats& st) {
+    if (STATS) st.c[ST_T_SPHERE + kind]++;
+    if (kind == RTW_GEOM_SPHERE) return sphere_t(w.spheres[idx], r, ts, te, t);
+    if (kind == RTW_GEOM_RECT) {
+        V3 pos;
+        return rect_t(load_rect(w, idx), r, ts, te, t, pos);
+    }
+    if (kind == RTW_GEOM_BOX) return box_t(w, idx, r, ts, te, t);
+    V3 pos;
+    float w0, w1, w2;
+    return tri_test(load_tri(w, idx), r, ts, te, t, pos, w0, w1, w2);
+}
+
+// ---------------------------------------------------------------------------------------------
+// leaf wrappers (hittable.rs:234-244, 271-292; transformations.rs:37-111)
+// ---------------------------------------------------------------------------------------------
+struct Xf {
+    V3 off;
+    float ys, yc;
+};
+__device__ __forceinline__ V3 rot_up(float c, float s, V3 v) {
+    return v3(c * v.x + s * v.z, v.y, -s * v.x + c * v.z);
+}
+__device__ __forceinline__ Ray xf_reverse(const Xf& x, const Ray& r) {
+    Ray o;
+    o.o = rot_up(x.yc, -x.ys, sub(r.o, x.off));
+    o.d = rot_up(x.yc, -x.ys, r.d);
+    o.time = r.time;
+    return o;
+}
+__device__ __forceinline__ Xf anim_xf(const DWorld& w, int leaf, float time) {
+    const float4 b = w.leaf_xf[3 * leaf + 1], c = w.leaf_xf[3 * leaf + 2];
+    const V3 vt = mul(v3(b.z, b.w, c.x), time);
+    return Xf{v3(0.0f + vt.x, 0.0f + vt.y, 0.0f + vt.z), 0.0f, 1.0f};
+}
+__device__ __forceinline__ Xf leaf_xform(const DWorld& w, int leaf) {
+    const float4 a = w.leaf_xf[3 * leaf], b = w.leaf_xf[3 * leaf + 1];
+    return Xf{v3(a.y, a.z, a.w), b.x, b.y};
+}
+// the ray as seen by the leaf's primitive
+__device__ __forceinline__ Ray leaf_local_ray(const DWorld& w, int leaf, uint32_t flags, const Ray& r) {
+    Ray rr = r;
+    if (flags & RTW_LEAF_ANIMATION) rr = xf_reverse(anim_xf(w, leaf, r.time), rr);
+    if (flags & RTW_LEAF_TRANSFORM) rr = xf_reverse(leaf_xform(w, leaf), rr);
+    return rr;
+}
+
+// SceneElement::hit for one leaf (candidate test: t only).  Volumes draw one f32 here.
+template <bool STATS>
+__device__ __forceinline__ bool leaf_t(const DWorld& w, int leaf, const Ray& r, float ts, float te, rtw_xoro& rng,
+                                       float& t, Stats& st) {
+    const int4 info = w.leaf_info[leaf];
+    const uint32_t flags = (uint32_t)info.w;
+    const Ray rr = (flags & (RTW_LEAF_ANIMATION | RTW_LEAF_TRANSFORM)) ? leaf_local_ray(w, leaf, flags, r) : r;
+    const bool volume = (flags & RTW_LEAF_VOLUME) != 0;
+    // VolumeGeometry::hit (hittable.rs:309-331): boundary hit over (-inf, inf), then from t0+0.001
+    float lo = volume ? -F32_INF : ts, hi = volume ? F32_INF : te;
+    float t0 = 0.0f;
+    for (int pass = 0;; ++pass) {
+        float tt;
+        if (!geom_t<STATS>(w, info.x, info.y, rr, lo, hi, tt, st)) return false;
+        if (!volume) {
+            t = tt;
+            return true;
+        }
+        if (pass == 0) {
+            t0 = tt;
+            lo = t0 + 0.001f;
+            continue;
+        }
+        const float sm = rtw_maxr(t0, ts);
+        const float em = rtw_minr(tt, te);
+        if (sm >= em) return false;
+        const float nid = w.leaf_xf[3 * leaf].x;
+        const float tv = rtw_maxr(sm, 0.0f) + nid * d_logf(rtw_gen_f32(&rng));
+        if (tv > em) return false;
+        t = tv;
+        return true;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// hit record of the closest leaf (hittable.rs:24-102 + the primitives' record parts)
+// ---------------------------------------------------------------------------------------------
+struct Hit {
+    V3 pos, n;
+    float u, v;
+    bool front;
+    int material;
+};
+__device__ __forceinline__ void from_ray(Hit& h, const Ray& r, V3 pos, V3 sn, float u, float v) {
+    h.front = dot(sn, r.d) < 0.0f;  // hittable.rs:41-46
+    h.n = h.front ? sn : neg(sn);
+    h.pos = pos;
+    h.u = u;
+    h.v = v;
+}
+__device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray& r, float t, Hit& h) {
+    const int4 info = w.leaf_info[leaf];
+    const uint32_t flags = (uint32_t)info.w;
+    const Ray rr = leaf_local_ray(w, leaf, flags, r);
+    const int kind = info.x, idx = info.y;
+    if (flags & RTW_LEAF_VOLUME) {  // hittable.rs:333-340
+        h.pos = at(rr, t);
+        h.n = v3(0.0f, 1.0f, 0.0f);
+        h.u = 0.0f;
+        h.v = 0.0f;
+        h.front = false;
+    } else if (kind == RTW_GEOM_SPHERE) {  // sphere_geometry.rs:42-52
+        const float4 s = w.spheres[idx];
+        const V3 pos = at(rr, t);
+        const V3 sn = divs(sub(pos, v3(s.x, s.y, s.z)), s.w);
+        const float theta = d_acosf(sn.y);  // vec3.rs:241-249
+        const float phi = d_atan2f(-sn.z, sn.x) + F32_PI;
+        from_ray(h, rr, pos, sn, phi / F32_TAU, theta / F32_PI);
+    } else if (kind == RTW_GEOM_RECT) {  // rect_geometry.rs:37-55
+        const RectG g = load_rect(w, idx);
+        int p0, p1, n;
+        rect_axes(g.plane, p0, p1, n);
+        const V3 pos = add(rr.o, mul(rr.d, t));
+        const float u = (comp(pos, p0) - g.r00) / (g.r01 - g.r00);
+        const float v = (comp(pos, p1) - g.r10) / (g.r01 - g.r10);  // the :45 typo
+        V3 sn = v3(0.0f, 0.0f, 0.0f);
+        setc(sn, n, -1.0f);
+        from_ray(h, rr, pos, sn, u, v);
+    } else if (kind == RTW_GEOM_BOX) {  // aabb.rs:80-101
+        const float4 ba = w.boxes[2 * idx], bb = w.boxes[2 * idx + 1];
+        float nt, ft;
+        int np, fp;
+        box_line(ba, bb, rr, nt, np, ft, fp);
+        const int plane = (t == nt) ? np : fp;
+        const V3 pos = add(rr.o, mul(rr.d, t));
+        const V3 bmin = v3(ba.x, ba.y, ba.z), bmax = v3(ba.w, bb.x, bb.y);
+        const float center = (comp(bmax, plane) + comp(bmin, plane)) * 0.5f;
+        V3 sn = v3(0.0f, 0.0f, 0.0f);
+        setc(sn, plane, rtw_signum(comp(pos, plane) - center));
+        from_ray(h, rr, pos, sn, 0.0f, 0.0f);
+    } else {  // triangle_geometry.rs:22-39
+        const TriP T = load_tri(w, idx);
+        float w0, w1, w2;
+        const V3 pos = at(rr, t);
+        {
+            // recompute barycentrics from the final t exactly as the test did
+            const V3 dir1 = sub(T.p1, T.p0);
+            const V3 dir2 = sub(T.p2, T.p0);
+            const V3 normal = unit(cross(dir1, dir2));
+            const V3 q = sub(pos, T.p0);
+            V3 vt = cross(normal, dir2);
+            w1 = dot(q, vt) / dot(dir1, vt);
+            vt = cross(normal, dir1);
+            w2 = dot(q, vt) / dot(dir2, vt);
+            w0 = 1.0f - w1 - w2;
+        }
+        const float4 a0 = w.tri_attr[4 * idx], a1 = w.tri_attr[4 * idx + 1], a2 = w.tri_attr[4 * idx + 2],
+                     a3 = w.tri_attr[4 * idx + 3];
+        const V3 n0 = v3(a0.x, a0.y, a0.z), n1 = v3(a0.w, a1.x, a1.y), n2 = v3(a1.z, a1.w, a2.x);
+        const float u0 = a2.y, v0 = a2.z, u1 = a2.w, v1 = a3.x, u2 = a3.y, v2 = a3.z;
+        const float u = u0 * w0 + u1 * w1 + u2 * w2;  // math.rs:9-16
+        const float v = v0 * w0 + v1 * w1 + v2 * w2;
+        const V3 sn = add(add(mul(n0, w0), mul(n1, w1)), mul(n2, w2));
+        from_ray(h, rr, pos, sn, u, v);
+    }
+    // apply_hit_interaction, innermost wrapper first (hittable.rs:279-283)
+    if (flags & RTW_LEAF_TRANSFORM) {
+        const Xf x = leaf_xform(w, leaf);
+        h.pos = add(rot_up(x.yc, x.ys, h.pos), x.off);
+        h.n = rot_up(x.yc, x.ys, h.n);
+    }
+    if (flags & RTW_LEAF_ANIMATION) {
+        const Xf x = anim_xf(w, leaf, r.time);
+        h.pos = add(rot_up(x.yc, x.ys, h.pos), x.off);
+        h.n = rot_up(x.yc, x.ys, h.n);
+    }
+    h.material = info.z;
+}
+
+// ---------------------------------------------------------------------------------------------
+// BVH traversal (hittable.rs:429-473; aabb.rs:65-78)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool slab_axis(float mn, float mx, float o, float d, float ts, float te) {
+    const float a = (mn - o) / d;
+    const float b = (mx - o) / d;
+    const float t0 = (a < b) ? a : b;  // math.rs:35-41 minmax
+    const float t1 = (a < b) ? b : a;
+    const float tmin = rtw_maxr(t0, ts);
+    const float tmax = rtw_minr(t1, te);
+    return !(tmax <= tmin);
+}
+
+// Closest hit.  Returns the leaf index or -1; `te` is shrunk to the hit's t.
+template <bool STATS>
+__device__ __forceinline__ int trace(const DWorld& w, const Ray& r, float ts, float& te, rtw_xoro& rng, int32_t* stack,
+                                     Stats& st) {
+    int found = -1;
+    int32_t node = w.root;
+    int sp = 0;
+    for (;;) {
+        if (node < 0) {
+            const int leaf = -1 - node;
+            float t;
+            if (leaf_t<STATS>(w, leaf, r, ts, te, rng, t, st)) {
+                te = t;
+                found = leaf;
+            }
+        } else {
+            if (STATS) st.c[ST_NODES]++;
+            const float4 a = w.node_a[node];
+            const float4 b = w.node_b[node];
+            if (slab_axis(a.x, a.w, r.o.x, r.d.x, ts, te) && slab_axis(a.y, b.x, r.o.y, r.d.y, ts, te) &&
+                slab_axis(a.z, b.y, r.o.z, r.d.z, ts, te)) {
+                const int32_t lbits = __float_as_int(b.z);
+                const int32_t left = lbits >> 2;
+                const int axis = lbits & 3;
+                const int32_t right = __float_as_int(b.w);
+                const bool fwd = comp(r.d, axis) > 0.0f;
+                stack[(sp++) * RTW_BLOCK] = fwd ? right : left;
+                node = fwd ? left : right;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        node = stack[(--sp) * RTW_BLOCK];
+    }
+    return found;
+}
+
+// ---------------------------------------------------------------------------------------------
+// textures / materials / light / background
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float perlin_noise(const float* ranvec, const uint32_t* px, int bits, V3 p) {  // perlin.rs:48-91
+    const uint32_t mask = (1u << bits) - 1u;
+    const uint32_t* py = px + 256;
+    const uint32_t* pz = px + 512;
+    const float fx = __builtin_floorf(p.x), fy = __builtin_floorf(p.y), fz = __builtin_floorf(p.z);
+    const float u = p.x - fx, v = p.y - fy, ww = p.z - fz;
+    const uint32_t i = (uint32_t)rtw_f2i32_sat(fx), j = (uint32_t)rtw_f2i32_sat(fy), k = (uint32_t)rtw_f2i32_sat(fz);
+    const float uu = u * u * (3.0f - 2.0f * u);
+    const float vv = v * v * (3.0f - 2.0f * v);
+    const float wwx = ww * ww * (3.0f - 2.0f * ww);
+    float accum = 0.0f;
+    for (int q = 0; q < 8; ++q) {
+        const int a = q >> 2, b = (q >> 1) & 1, c = q & 1;
+        const uint32_t idx = px[(i + (uint32_t)a) & mask] ^ py[(j + (uint32_t)b) & mask] ^ pz[(k + (uint32_t)c) & mask];
+        const V3 cv = ld3(ranvec + 3 * idx);
+        const float fa = (float)a, fb = (float)b, fc = (float)c;
+        const V3 weight = v3(u - fa, v - fb, ww - fc);
+        accum += (fa * uu + (1.0f - fa) * (1.0f - uu)) * (fb * vv + (1.0f - fb) * (1.0f - vv)) *
+                 (fc * wwx + (1.0f - fc) * (1.0f - wwx)) * dot(cv, weight);
+    }
+    return accum;
+}
+
+// Marble (texture.rs:44-51) with turbulence(p, 7, 0.5) (perlin.rs:37-47); rare, kept out of line
+__device__ __forceinline__ float marble_k(const float* ranvec, const uint32_t* perm, int bits, float px, float py, float pz,
+                                       float scale) {
+    float acc = 0.0f, weight = 1.0f;
+    V3 p = v3(px, py, pz);
+    for (int i = 0; i < 7; ++i) {
+        acc += weight * perlin_noise(ranvec, perm, bits, p);
+        weight *= 0.5f;
+        p = mul(p, 2.0f);
+    }
+    const float turb = __builtin_fabsf(acc);
+    return 1.0f + d_sinf(pz * scale + 10.0f * turb);
+}
+
+template <bool STATS>
+__device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit& h, Stats& st) {  // texture.rs:23-53
+    for (int guard = 0; guard < 64; ++guard) {
+        const int4 t0 = w.textures[3 * tex];
+        const int kind = t0.x;
+        if (kind == RTW_TEX_SOLID) return v3(__int_as_float(t0.y), __int_as_float(t0.z), __int_as_float(t0.w));
+        const int4 t1 = w.textures[3 * tex + 1];
+        if (kind == RTW_TEX_CHECKER) {
+            const float f = __int_as_float(t1.x);
+            const V3 s = mul(h.pos, f);
+            const float sines = d_sinf(s.x) * d_sinf(s.y) * d_sinf(s.z);
+            tex = (sines < 0.0f) ? t1.y : t1.z;
+            continue;
+        }
+        const int4 t2 = w.textures[3 * tex + 2];
+        if (kind == RTW_TEX_IMAGE) {
+            const int4 im = w.images[t2.y];
+            uint32_t pu = rtw_f2u32_sat(h.u * (float)im.y);
+            uint32_t pv = rtw_f2u32_sat(h.v * (float)im.z);
+            pu = min(pu, (uint32_t)(im.y - 1));
+            pv = min(pv, (uint32_t)(im.z - 1));
+            if (STATS) st.c[ST_TEXEL]++;
+            const uint32_t px = w.texels[(size_t)im.x + (size_t)pv * (size_t)im.y + pu];
+            return v3((float)(px & 255u) / 255.0f, (float)((px >> 8) & 255u) / 255.0f,
+                      (float)((px >> 16) & 255u) / 255.0f);
+        }
+        const int pi = t2.x;
+        const float k = marble_k(w.perlin_ranvec + 768 * pi, w.perlin_perm + 768 * pi, w.perlin_bits[pi], h.pos.x,
+                                 h.pos.y, h.pos.z, __int_as_float(t1.w));
+        return mul(mul(v3(1.0f, 1.0f, 1.0f), 0.5f), k);
+    }
+    return v3(0.0f, 0.0f, 0.0f);
+}
+
+// rect_geometry.rs:60-85 (the light sampler)
+__device__ __forceinline__ V3 light_generate(const rtw_rect& g, V3 origin, rtw_xoro& rng) {
+    int p0, p1, n;
+    rect_axes(g.plane, p0, p1, n);
+    V3 e = v3(0.0f, 0.0f, 0.0f);
+    setc(e, p0, rtw_gen_range_f32(g.r0[0], g.r0[1], &rng));
+    setc(e, p1, rtw_gen_range_f32(g.r1[0], g.r1[1], &rng));
+    setc(e, n, g.dist);
+    return unit(sub(e, origin));
+}
+__device__ __forceinline__ float light_value(const rtw_rect& lg, V3 origin, V3 dir) {
+    Ray r;
+    r.o = origin;
+    r.d = dir;
+    r.time = 0.0f;
+    const RectG g{lg.plane, lg.dist, lg.r0[0], lg.r0[1], lg.r1[0], lg.r1[1]};
+    float t;
+    V3 pos;
+    if (!rect_t(g, r, 0.001f, F32_INF, t, pos)) return 0.0f;
+    int p0, p1, n;
+    rect_axes(g.plane, p0, p1, n);
+    V3 sn = v3(0.0f, 0.0f, 0.0f);
+    setc(sn, n, -1.0f);
+    const V3 hn = (dot(sn, dir) < 0.0f) ? sn : neg(sn);
+    const float area = (g.r01 - g.r00) * (g.r11 - g.r10);
+    const float dsq = t * t;
+    const float cosine = __builtin_fabsf(dot(hn, dir));
+    return dsq / (cosine * area);
+}
+
+__device__ __forceinline__ V3 background(const rtw_background& bg, V3 d) {  // background_color.rs:9-19
+    if (bg.kind == RTW_BG_SKY) {
+        const float t = 0.5f * (dot(v3(0.0f, 1.0f, 0.0f), d) + 1.0f);
+        return add(mul(v3(1.0f, 1.0f, 1.0f), 1.0f - t), mul(v3(0.5f, 0.7f, 1.0f), t));
+    }
+    return v3(bg.color[0], bg.color[1], bg.color[2]);
+}
+
+// Camera::ray (camera.rs:175-200)
+__device__ __forceinline__ Ray camera_ray(const rtw_camera& c, rtw_xoro& rng, float px, float py) {
+    V3 off = v3(0.0f, 0.0f, 0.0f);
+    if (c.lens_radius > 0.0f) {
+        float d[2];
+        rtw_unit_disc(&rng, d);
+        off = mul(add(mul(ld3(c.unit_right), d[0]), mul(ld3(c.unit_up), d[1])), c.lens_radius);
+    }
+    float start;
+    if (c.time0 == c.time1) start = c.time0;
+    else start = rtw_gen_range_f32(c.time0, c.time1, &rng);
+    Ray r;
+    r.time = start + (c.shutter_pace[0] * px + c.shutter_pace[1] * py);
+    r.o = add(ld3(c.position), off);
+    r.d = unit(sub(sub(add(ld3(c.upper_left_corner), mul(ld3(c.scaled_right), px)), mul(ld3(c.scaled_up), py)), off));
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// the megakernel
+// ---------------------------------------------------------------------------------------------
+template <bool STATS>
+__global__ __launch_bounds__(RTW_BLOCK) void render_kernel(KArgs A) {
+    __shared__ int32_t s_stack[RTW_STACK * RTW_BLOCK];
+    const int lane = threadIdx.x & 63;
+    const int64_t job = (int64_t)blockIdx.x * RTW_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (job >= A.jobs) return;
+    const int32_t local_tile = (int32_t)(job / A.chunks_per_tile);
+    const int32_t chunk = (int32_t)(job % A.chunks_per_tile);
+    const int32_t tile = A.part_index + local_tile * A.part_count;
+    const int32_t in_tile = chunk * 64 + lane;
+    if (in_tile >= A.tile_w * A.tile_h) return;
+    const int32_t px = (tile % A.tiles_x) * A.tile_w + in_tile % A.tile_w;
+    const int32_t py = (tile / A.tiles_x) * A.tile_h + in_tile / A.tile_w;
+    if (px >= A.width || py >= A.height) return;
+
+    const DWorld& w = A.w;
+    int32_t* stack = s_stack + threadIdx.x;
+    Stats st;
+    if (STATS)
+        for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
+
+    const uint32_t pix = (uint32_t)(py * A.width + px);
+    const float fx = (float)px * A.sx, fy = (float)py * A.sy;  // size2i.rs:52-55
+
+    V3 sum = v3(0.0f, 0.0f, 0.0f);
+    uint32_t sample = 0;
+    rtw_xoro rng;
+    Ray ray;
+    V3 pdir, att, acc;
+    int32_t depth;
+
+    // rendering.rs:174-176: jitter (x then y), then Camera::ray
+    auto start_sample = [&]() {
+        rng = rtw_sample_stream(A.seed_key, pix, sample);
+        const float jx = rtw_uniform_sample(&A.ux, &rng);
+        const float jy = rtw_uniform_sample(&A.uy, &rng);
+        ray = camera_ray(w.wc->cam, rng, fx + jx, fy + jy);
+        pdir = ray.d;
+        att = v3(1.0f, 1.0f, 1.0f);
+        acc = v3(0.0f, 0.0f, 0.0f);
+        depth = A.max_depth;
+    };
+    start_sample();
+
+    for (;;) {
+        V3 color;
+        bool done = false;
+        float te = F32_INF;
+        if (STATS) st.c[ST_RAYS]++;
+        const int leaf = trace<STATS>(w, ray, 0.001f, te, rng, stack, st);
+        if (leaf >= 0) {
+            if (STATS) {
+                st.c[ST_H_SPHERE + w.leaf_info[leaf].x]++;
+                st.c[ST_MAT]++;
+            }
+            Hit h;
+            leaf_record(w, leaf, ray, te, h);
+            if (A.mode == RTW_MODE_NORMALS) {  // rendering.rs:110-113
+                color = mul(add(h.n, v3(1.0f, 1.0f, 1.0f)), 0.5f);
+                done = true;
+            } else if (depth <= 1) {  // rendering.rs:26-27
+                color = v3(0.0f, 0.0f, 0.0f);
+                done = true;
+            } else {
+                const int4 M = w.materials[h.material];
+                const int mkind = M.x;
+                // Material::scatter (material.rs:52-114).  At most one texture lookup per bounce:
+                // the albedo of a scattering material or the emission of a DiffuseLight.
+                bool scatters = true;
+                bool cosine = false;      // MaterialScatteringDistribution::Cosine
+                bool need_sphere = false; // one UnitSphere draw site (Cosine / Isotropic)
+                int tex = -1;
+                V3 sdir = v3(0.0f, 0.0f, 0.0f);
+                if (mkind == RTW_MAT_LAMBERT) {
+                    tex = M.y;
+                    cosine = true;
+                } else if (mkind == RTW_MAT_METAL) {
+                    const float fuzz = __int_as_float(M.z);
+                    V3 fz = v3(0.0f, 0.0f, 0.0f);
+                    if (fuzz > 0.0f) {
+                        float b[3];
+                        rtw_unit_ball(&rng, b);
+                        fz = mul(v3(b[0], b[1], b[2]), fuzz);
+                    }
+                    const V3 dir = add(reflect(ray.d, h.n), fz);
+                    if (dot(dir, h.n) > 0.0f) {
+                        sdir = unit(dir);
+                        tex = M.y;
+                    } else {
+                        scatters = false;
+                    }
+                } else if (mkind == RTW_MAT_DIELECTRIC) {
+                    const float ior = __int_as_float(M.w);
+                    const float ratio = h.front ? (1.0f / ior) : ior;
+                    const float cos_t = rtw_minr(dot(neg(ray.d), h.n), 1.0f);
+                    const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+                    bool refl = ratio * sin_t > 1.0f;
+                    if (!refl) {
+                        const float r0 = (1.0f - ratio) / (1.0f + ratio);
+                        const float rs = r0 * r0;
+                        const float x = 1.0f - cos_t;
+                        const float x2 = x * x;
+                        const float p5 = x * (x2 * x2);  // powi(5)
+                        refl = (rs + (1.0f - rs) * p5) > rtw_gen_f32(&rng);
+                    }
+                    sdir = unit(refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio));
+                } else if (mkind == RTW_MAT_ISOTROPIC) {
+                    need_sphere = true;
+                    tex = M.y;
+                } else {
+                    scatters = false;  // DiffuseLight: emit
+                    tex = M.y;
+                }
+                // sample_final_scattering_distribution (rendering.rs:73-92): the mixture draws its
+                // bool before either generator.
+                bool light_dir = false;
+                if (cosine) {
+                    if (w.has_light) light_dir = rtw_gen_bool_half(&rng);
+                    need_sphere = !light_dir;
+                }
+                if (light_dir) sdir = light_generate(w.wc->light, h.pos, rng);
+                if (need_sphere) {
+                    float s[3];
+                    rtw_unit_sphere(&rng, s);
+                    const V3 sv = v3(s[0], s[1], s[2]);
+                    if (cosine) {  // (n + UnitSphere).unit_or_else(n) (material.rs:20-22)
+                        const V3 v = add(h.n, sv);
+                        const float lsq = dot(v, v);
+                        sdir = (lsq > 1e-8f) ? divs(v, __builtin_sqrtf(lsq)) : h.n;
+                    } else {
+                        sdir = sv;
+                    }
+                }
+                const V3 tc = (tex >= 0) ? texture_sample<STATS>(w, tex, h, st) : v3(0.0f, 0.0f, 0.0f);
+                const V3 emitted = (mkind == RTW_MAT_DIFFUSE_LIGHT) ? tc : v3(0.0f, 0.0f, 0.0f);
+                const V3 albedo = (mkind == RTW_MAT_DIELECTRIC) ? v3(1.0f, 1.0f, 1.0f) : tc;
+                if (scatters) {
+                    float prob = 1.0f;
+                    if (cosine) {
+                        const float mv = rtw_maxr(dot(h.n, sdir), 0.0f) / F32_PI;  // Cosine::value
+                        float p = mv;
+                        if (w.has_light) p = 0.5f * light_value(w.wc->light, h.pos, sdir) + (1.0f - 0.5f) * mv;
+                        const float spdf = rtw_maxr(dot(h.n, sdir), 0.0f) / F32_PI;  // material.rs:123-127
+                        prob = spdf / p;
+                    }
+                    acc = add(acc, conv(att, emitted));
+                    att = mul(conv(att, albedo), prob);
+                    ray.o = h.pos;
+                    ray.d = sdir;
+                    depth -= 1;
+                } else {
+                    color = add(acc, conv(att, emitted));
+                    done = true;
+                }
+            }
+        } else {
+            // rendering.rs:67 (background of the PRIMARY ray) / :114
+            color = add(acc, conv(att, background(w.wc->bg, pdir)));
+            done = true;
+        }
+        if (done) {
+            sum = add(sum, color);
+            if (STATS) st.c[ST_SAMPLES]++;
+            ++sample;
+            if (sample >= A.spp) break;
+            start_sample();
+        }
+    }
+    const V3 pixel = divs(sum, (float)A.spp);
+    if (STATS) {
+        for (int i = 0; i < ST_COUNT; ++i)
+            if (st.c[i]) atomicAdd(&A.stats[i], (unsigned long long)st.c[i]);
+    }
+    float* o;
+    if (A.layout == RTW_LAYOUT_TILES)
+        o = A.out + ((int64_t)local_tile * A.tile_w * A.tile_h + in_tile) * 3;
+    else
+        o = A.out + (int64_t)pix * 3;
+    o[0] = pixel.x;
+    o[1] = pixel.y;
+    o[2] = pixel.z;
+}
+
+// scatter gathered tile buffers back into the image
+__global__ void untile_kernel(const float* tiles, int64_t stride, float* image, int32_t width, int32_t height,
+                              int32_t tile_w, int32_t tile_h, int32_t tiles_x, int32_t n_tiles, int32_t part_count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = (int64_t)tile_w * tile_h;
+    if (i >= (int64_t)n_tiles * per_tile) return;
+    const int32_t tile = (int32_t)(i / per_tile);
+    const int32_t in_tile = (int32_t)(i % per_tile);
+    const int32_t px = (tile % tiles_x) * tile_w + in_tile % tile_w;
+    const int32_t py = (tile / tiles_x) * tile_h + in_tile / tile_w;
+    if (px >= width || py >= height) return;
+    const int32_t part = tile % part_count, local = tile / part_count;
+    const float* src = tiles + (int64_t)part * stride + ((int64_t)local * per_tile + in_tile) * 3;
+    float* dst = image + ((int64_t)py * width + px) * 3;
+    dst[0] = src[0];
+    dst[1] = src[1];
+    dst[2] = src[2];
+}
+
+// color.rs:43-48 to_rgb8_gamma2
+__global__ void encode_kernel(const float* img, int64_t n, uint8_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * 3) return;
+    const float v = rtw_clampr(0.0f, 255.0f, __builtin_sqrtf(img[i]) * 256.0f);
+    out[i] = rtw_f2u8_sat(v);
+}
+
+__global__ void eval_scalar_kernel(int fn, const float* a, const float* b, int64_t n, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float r;
+    switch (fn) {
+        case 0: r = rtw_acosf(a[i]); break;
+        case 1: r = rtw_atan2f(a[i], b[i]); break;
+        case 2: r = rtw_logf(a[i]); break;
+        case 3: r = rtw_sinf(a[i]); break;
+        case 4: r = a[i] / b[i]; break;
+        case 5: r = __builtin_sqrtf(a[i]); break;
+        default: r = a[i] / b[i]; break;
+    }
+    out[i] = r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+#define HIP_TRY(expr)                                                                             \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            return rtw::fail(RTW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));    \
+    } while (0)
+
+inline uint32_t fbits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+inline float ibits(int32_t i) {
+    float f;
+    std::memcpy(&f, &i, 4);
+    return f;
+}
+
+struct Layout {
+    std::vector<uint8_t> blob;
+    size_t push(const void* p, size_t bytes) {
+        size_t off = (blob.size() + 255) & ~(size_t)255;
+        blob.resize(off + bytes);
+        if (bytes) std::memcpy(blob.data() + off, p, bytes);
+        return off;
+    }
+};
+
+int check_world(const rtw_world* w, int* depth_out) {
+    if (!w) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null world");
+    if (w->leaf_count < 1) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "world has no leaves");
+    auto bad = [&](const char* m) { return rtw::fail(RTW_ERR_INVALID_ARGUMENT, std::string("invalid world: ") + m); };
+    if (w->root >= 0 ? w->root >= w->node_count : (-1 - w->root) >= w->leaf_count) return bad("root out of range");
+    for (int i = 0; i < w->leaf_count; ++i) {
+        const rtw_leaf& L = w->leaves[i];
+        const int counts[4] = {w->sphere_count, w->rect_count, w->box_count, w->triangle_count};
+        if (L.geom_kind < 0 || L.geom_kind > 3) return bad("leaf geometry kind");
+        if (L.geom_index < 0 || L.geom_index >= counts[L.geom_kind]) return bad("leaf geometry index");
+        if (L.material < 0 || L.material >= w->material_count) return bad("leaf material index");
+    }
+    for (int i = 0; i < w->material_count; ++i) {
+        const rtw_material& m = w->materials[i];
+        if (m.kind < 0 || m.kind > 4) return bad("material kind");
+        if (m.kind != RTW_MAT_DIELECTRIC && (m.texture < 0 || m.texture >= w->texture_count)) return bad("material texture");
+    }
+    for (int i = 0; i < w->texture_count; ++i) {
+        const rtw_texture& t = w->textures[i];
+        if (t.kind == RTW_TEX_CHECKER && (t.even < 0 || t.even >= w->texture_count || t.odd < 0 || t.odd >= w->texture_count))
+            return bad("checker texture ids");
+        if (t.kind == RTW_TEX_IMAGE && (t.image < 0 || t.image >= w->image_count)) return bad("image id");
+        if (t.kind == RTW_TEX_MARBLE && (t.perlin < 0 || t.perlin >= w->perlin_count)) return bad("perlin id");
+    }
+    for (int i = 0; i < w->perlin_count; ++i)
+        if (w->perlins[i].bits < 1 || w->perlins[i].bits > 8) return bad("perlin bits");
+    for (int i = 0; i < w->image_count; ++i)
+        if (w->images[i].width < 1 || w->images[i].height < 1 || !w->images[i].rgb) return bad("image");
+    // node references + depth (the per-lane stack holds RTW_STACK entries)
+    std::vector<std::pair<int32_t, int>> todo;
+    int maxd = 0;
+    std::vector<uint8_t> seen((size_t)std::max(1, w->node_count), 0);
+    if (w->root >= 0) todo.emplace_back(w->root, 0);
+    while (!todo.empty()) {
+        auto [n, d] = todo.back();
+        todo.pop_back();
+        if (n < 0) {
+            if (-1 - n >= w->leaf_count) return bad("leaf reference");
+            continue;
+        }
+        if (n >= w->node_count || seen[(size_t)n]) return bad("node reference");
+        seen[(size_t)n] = 1;
+        const rtw_bvh_node& nd = w->nodes[n];
+        if (nd.axis < 0 || nd.axis > 2) return bad("node axis");
+        maxd = std::max(maxd, d + 1);
+        todo.emplace_back(nd.left, d + 1);
+        todo.emplace_back(nd.right, d + 1);
+    }
+    if (maxd > RTW_STACK) return rtw::fail(RTW_ERR_UNSUPPORTED, "BVH deeper than the device stack");
+    *depth_out = maxd;
+    return RTW_OK;
+}
+
+}  // namespace
+
+struct rtw_gpu_world {
+    int device = 0;
+    void* arena = nullptr;
+    DWorld w{};
+};
+
+extern "C" RTW_API int rtw_device_count(int* count) {
+    if (!count) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_world** out) {
+    if (!out) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null out");
+    int depth = 0;
+    const int v = check_world(w, &depth);
+    if (v != RTW_OK) return v;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device: the MI355X path requires a GPU (there is no CPU fallback)");
+    if (device < 0 || device >= ndev) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+
+    Layout L;
+    // nodes
+    std::vector<float4> na((size_t)std::max(1, w->node_count)), nb((size_t)std::max(1, w->node_count));
+    for (int i = 0; i < w->node_count; ++i) {
+        const rtw_bvh_node& n = w->nodes[i];
+        na[(size_t)i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
+        nb[(size_t)i] = make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
+    }
+    const size_t o_na = L.push(na.data(), na.size() * sizeof(float4));
+    const size_t o_nb = L.push(nb.data(), nb.size() * sizeof(float4));
+    // leaves
+    std::vector<int4> li((size_t)w->leaf_count);
+    std::vector<float4> lx((size_t)w->leaf_count * 3);
+    for (int i = 0; i < w->leaf_count; ++i) {
+        const rtw_leaf& l = w->leaves[i];
+        li[(size_t)i] = make_int4(l.geom_kind, l.geom_index, l.material, (int)l.flags);
+        lx[3 * (size_t)i] = make_float4(l.neg_inv_density, l.offset[0], l.offset[1], l.offset[2]);
+        lx[3 * (size_t)i + 1] = make_float4(l.y_sin, l.y_cos, l.velocity[0], l.velocity[1]);
+        lx[3 * (size_t)i + 2] = make_float4(l.velocity[2], 0.0f, 0.0f, 0.0f);
+    }
+    const size_t o_li = L.push(li.data(), li.size() * sizeof(int4));
+    const size_t o_lx = L.push(lx.data(), lx.size() * sizeof(float4));
+    // primitives
+    std::vector<float4> sp((size_t)w->sphere_count);
+    for (int i = 0; i < w->sphere_count; ++i) {
+        const rtw_sphere& s = w->spheres[i];
+        sp[(size_t)i] = make_float4(s.center[0], s.center[1], s.center[2], s.radius);
+    }
+    std::vector<float4> rc((size_t)w->rect_count * 2);
+    for (int i = 0; i < w->rect_count; ++i) {
+        const rtw_rect& r = w->rects[i];
+        rc[2 * (size_t)i] = make_float4(r.dist, r.r0[0], r.r0[1], r.r1[0]);
+        rc[2 * (size_t)i + 1] = make_float4(r.r1[1], ibits(r.plane), 0.0f, 0.0f);
+    }
+    std::vector<float4> bx((size_t)w->box_count * 2);
+    for (int i = 0; i < w->box_count; ++i) {
+        const rtw_box& b = w->boxes[i];
+        bx[2 * (size_t)i] = make_float4(b.min[0], b.min[1], b.min[2], b.max[0]);
+        bx[2 * (size_t)i + 1] = make_float4(b.max[1], b.max[2], 0.0f, 0.0f);
+    }
+    std::vector<float4> tp((size_t)w->triangle_count * 3), ta((size_t)w->triangle_count * 4);
+    for (int i = 0; i < w->triangle_count; ++i) {
+        const rtw_triangle& t = w->triangles[i];
+        const float (*p)[3] = t.positions;
+        tp[3 * (size_t)i] = make_float4(p[0][0], p[0][1], p[0][2], p[1][0]);
+        tp[3 * (size_t)i + 1] = make_float4(p[1][1], p[1][2], p[2][0], p[2][1]);
+        tp[3 * (size_t)i + 2] = make_float4(p[2][2], 0.0f, 0.0f, 0.0f);
+        const float (*n)[3] = t.normals;
+        const float (*u)[2] = t.uvs;
+        ta[4 * (size_t)i] = make_float4(n[0][0], n[0][1], n[0][2], n[1][0]);
+        ta[4 * (size_t)i + 1] = make_float4(n[1][1], n[1][2], n[2][0], n[2][1]);
+        ta[4 * (size_t)i + 2] = make_float4(n[2][2], u[0][0], u[0][1], u[1][0]);
+        ta[4 * (size_t)i + 3] = make_float4(u[1][1], u[2][0], u[2][1], 0.0f);
+    }
+    const size_t o_sp = L.push(sp.data(), sp.size() * sizeof(float4));
+    const size_t o_rc = L.push(rc.data(), rc.size() * sizeof(float4));
+    const size_t o_bx = L.push(bx.data(), bx.size() * sizeof(float4));
+    const size_t o_tp = L.push(tp.data(), tp.size() * sizeof(float4));
+    const size_t o_ta = L.push(ta.data(), ta.size() * sizeof(float4));
+    // materials / textures / images / perlin
+    std::vector<int4> mt((size_t)w->material_count);
+    for (int i = 0; i < w->material_count; ++i) {
+        const rtw_material& m = w->materials[i];
+        mt[(size_t)i] = make_int4(m.kind, m.texture, (int)fbits(m.fuzz), (int)fbits(m.index_of_refraction));
+    }
+    std::vector<int4> tx((size_t)w->texture_count * 3);
+    for (int i = 0; i < w->texture_count; ++i) {
+        const rtw_texture& t = w->textures[i];
+        tx[3 * (size_t)i] = make_int4(t.kind, (int)fbits(t.color[0]), (int)fbits(t.color[1]), (int)fbits(t.color[2]));
+        tx[3 * (size_t)i + 1] = make_int4((int)fbits(t.inv_frequency), t.even, t.odd, (int)fbits(t.scale));
+        tx[3 * (size_t)i + 2] = make_int4(t.perlin, t.image, 0, 0);
+    }
+    std::vector<int4> im((size_t)std::max(1, w->image_count));
+    std::vector<uint32_t> texels;
+    for (int i = 0; i < w->image_count; ++i) {
+        const rtw_image& I = w->images[i];
+        im[(size_t)i] = make_int4((int)texels.size(), I.width, I.height, 0);
+        const size_t n = (size_t)I.width * (size_t)I.height;
+        for (size_t k = 0; k < n; ++k)
+            texels.push_back((uint32_t)I.rgb[3 * k] | ((uint32_t)I.rgb[3 * k + 1] << 8) | ((uint32_t)I.rgb[3 * k + 2] << 16));
+    }
+    if (texels.empty()) texels.push_back(0);
+    std::vector<float> pr((size_t)std::max(1, w->perlin_count) * 768);
+    std::vector<uint32_t> pp((size_t)std::max(1, w->perlin_count) * 768);
+    std::vector<int> pb((size_t)std::max(1, w->perlin_count));
+    for (int i = 0; i < w->perlin_count; ++i) {
+        const rtw_perlin& P = w->perlins[i];
+        std::memcpy(&pr[(size_t)i * 768], P.ranvec, sizeof(P.ranvec));
+        std::memcpy(&pp[(size_t)i * 768], P.perm_x, sizeof(P.perm_x));
+        std::memcpy(&pp[(size_t)i * 768 + 256], P.perm_y, sizeof(P.perm_y));
+        std::memcpy(&pp[(size_t)i * 768 + 512], P.perm_z, sizeof(P.perm_z));
+        pb[(size_t)i] = P.bits;
+    }
+    const size_t o_mt = L.push(mt.data(), mt.size() * sizeof(int4));
+    const size_t o_tx = L.push(tx.data(), tx.size() * sizeof(int4));
+    const size_t o_im = L.push(im.data(), im.size() * sizeof(int4));
+    const size_t o_te = L.push(texels.data(), texels.size() * sizeof(uint32_t));
+    const size_t o_pr = L.push(pr.data(), pr.size() * sizeof(float));
+    const size_t o_pp = L.push(pp.data(), pp.size() * sizeof(uint32_t));
+    const size_t o_pb = L.push(pb.data(), pb.size() * sizeof(int));
+    WorldConst wcst;
+    std::memset(&wcst, 0, sizeof(wcst));
+    wcst.cam = w->camera;
+    wcst.light = w->light;
+    wcst.bg = w->background;
+    const size_t o_wc = L.push(&wcst, sizeof(wcst));
+
+    auto* g = new rtw_gpu_world;
+    g->device = device;
+    hipError_t e = hipMalloc(&g->arena, L.blob.size());
+    if (e != hipSuccess) {
+        delete g;
+        return rtw::fail(RTW_ERR_OUT_OF_MEMORY, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    e = hipMemcpy(g->arena, L.blob.data(), L.blob.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(g->arena);
+        delete g;
+        return rtw::fail(RTW_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    }
+    uint8_t* base = (uint8_t*)g->arena;
+    DWorld& d = g->w;
+    d.node_a = (const float4*)(base + o_na);
+    d.node_b = (const float4*)(base + o_nb);
+    d.leaf_info = (const int4*)(base + o_li);
+    d.leaf_xf = (const float4*)(base + o_lx);
+    d.spheres = (const float4*)(base + o_sp);
+    d.rects = (const float4*)(base + o_rc);
+    d.boxes = (const float4*)(base + o_bx);
+    d.tri_pos = (const float4*)(base + o_tp);
+    d.tri_attr = (const float4*)(base + o_ta);
+    d.materials = (const int4*)(base + o_mt);
+    d.textures = (const int4*)(base + o_tx);
+    d.images = (const int4*)(base + o_im);
+    d.texels = (const uint32_t*)(base + o_te);
+    d.perlin_ranvec = (const float*)(base + o_pr);
+    d.perlin_perm = (const uint32_t*)(base + o_pp);
+    d.perlin_bits = (const int*)(base + o_pb);
+    d.root = w->root;
+    d.has_light = w->has_light;
+    d.wc = (const WorldConst*)(base + o_wc);
+    *out = g;
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_world_release(rtw_gpu_world* g) {
+    if (!g) return RTW_OK;
+    (void)hipSetDevice(g->device);
+    if (g->arena) (void)hipFree(g->arena);
+    delete g;
+    return RTW_OK;
+}
+
+namespace {
+
+int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
+    if (!g || !p) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    if (p->width < 2 || p->height < 2)  // rendering.rs:132-138 divides by (W-1), (H-1)
+        return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "image width and height must be >= 2");
+    if (p->samples_per_pixel < 1) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "samples_per_pixel must be >= 1");
+    if (p->render_mode != RTW_MODE_DEFAULT && p->render_mode != RTW_MODE_NORMALS)
+        return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "unknown render mode");
+    const int tw = p->tile_width > 0 ? p->tile_width : 8;
+    const int th = p->tile_height > 0 ? p->tile_height : 8;
+    const int pc = p->part_count > 0 ? p->part_count : 1;
+    if (p->part_index < 0 || p->part_index >= pc) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "part_index out of range");
+    std::memset(&A, 0, sizeof(A));
+    A.w = g->w;
+    A.width = p->width;
+    A.height = p->height;
+    A.spp = p->samples_per_pixel;
+    A.max_depth = p->max_depth;
+    A.mode = p->render_mode;
+    A.layout = p->layout;
+    A.tile_w = tw;
+    A.tile_h = th;
+    A.tiles_x = (p->width + tw - 1) / tw;
+    const int tiles_y = (p->height + th - 1) / th;
+    A.n_tiles = A.tiles_x * tiles_y;
+    A.part_index = p->part_index;
+    A.part_count = pc;
+    A.chunks_per_tile = (tw * th + 63) / 64;
+    const int64_t owned = A.n_tiles > p->part_index ? (A.n_tiles - p->part_index + pc - 1) / pc : 0;
+    A.jobs = owned * A.chunks_per_tile;
+    A.seed_key = rtw_seed_key(p->seed);
+    A.sx = 1.0f / (float)(p->width - 1);
+    A.sy = 1.0f / (float)(p->height - 1);
+    A.ux = rtw_uniform_new(0.0f, 1.0f / (float)(p->width - 1));
+    A.uy = rtw_uniform_new(0.0f, 1.0f / (float)(p->height - 1));
+    return RTW_OK;
+}
+
+}  // namespace
+
+extern "C" RTW_API int rtw_partition_floats(const rtw_render_params* p, int64_t* floats) {
+    if (!p || !floats) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    const int tw = p->tile_width > 0 ? p->tile_width : 8;
+    const int th = p->tile_height > 0 ? p->tile_height : 8;
+    const int pc = p->part_count > 0 ? p->part_count : 1;
+    if (p->width < 1 || p->height < 1 || p->part_index < 0 || p->part_index >= pc)
+        return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad params");
+    const int64_t n_tiles = (int64_t)((p->width + tw - 1) / tw) * ((p->height + th - 1) / th);
+    const int64_t owned = n_tiles > p->part_index ? (n_tiles - p->part_index + pc - 1) / pc : 0;
+    *floats = owned * tw * th * 3;
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_render_device(rtw_gpu_world* g, const rtw_render_params* p, float* d_out, void* stream) {
+    KArgs A;
+    const int v = make_args(g, p, A);
+    if (v != RTW_OK) return v;
+    if (!d_out) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null output");
+    A.out = d_out;
+    HIP_TRY(hipSetDevice(g->device));
+    if (A.jobs == 0) return RTW_OK;
+    const int64_t blocks = (A.jobs + RTW_WAVES_PER_BLOCK - 1) / RTW_WAVES_PER_BLOCK;
+    hipLaunchKernelGGL(render_kernel<false>, dim3((unsigned)blocks), dim3(RTW_BLOCK), 0, (hipStream_t)stream, A);
+    HIP_TRY(hipGetLastError());
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_render_collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s) {
+    KArgs A;
+    const int v = make_args(g, p, A);
+    if (v != RTW_OK) return v;
+    if (!s) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null stats");
+    HIP_TRY(hipSetDevice(g->device));
+    float* out = nullptr;
+    unsigned long long* st = nullptr;
+    HIP_TRY(hipMalloc(&out, (size_t)p->width * p->height * 3 * sizeof(float)));
+    HIP_TRY(hipMalloc(&st, ST_COUNT * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(st, 0, ST_COUNT * sizeof(unsigned long long)));
+    A.out = out;
+    A.layout = RTW_LAYOUT_IMAGE;
+    A.stats = st;
+    const int64_t blocks = (A.jobs + RTW_WAVES_PER_BLOCK - 1) / RTW_WAVES_PER_BLOCK;
+    if (blocks > 0) hipLaunchKernelGGL(render_kernel<true>, dim3((unsigned)blocks), dim3(RTW_BLOCK), 0, 0, A);
+    HIP_TRY(hipGetLastError());
+    unsigned long long h[ST_COUNT];
+    HIP_TRY(hipMemcpy(h, st, sizeof(h), hipMemcpyDeviceToHost));
+    (void)hipFree(out);
+    (void)hipFree(st);
+    s->samples = h[ST_SAMPLES];
+    s->rays = h[ST_RAYS];
+    s->node_visits = h[ST_NODES];
+    s->sphere_tests = h[ST_T_SPHERE];
+    s->rect_tests = h[ST_T_RECT];
+    s->box_tests = h[ST_T_BOX];
+    s->triangle_tests = h[ST_T_TRI];
+    s->sphere_hits = h[ST_H_SPHERE];
+    s->rect_hits = h[ST_H_RECT];
+    s->box_hits = h[ST_H_BOX];
+    s->triangle_hits = h[ST_H_TRI];
+    s->material_reads = h[ST_MAT];
+    s->texel_reads = h[ST_TEXEL];
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_render(const rtw_world* w, const rtw_render_params* p, int device, float* out_rgb) {
+    if (!p || !out_rgb) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    rtw_gpu_world* g = nullptr;
+    int rc = rtw_world_upload(w, device, &g);
+    if (rc != RTW_OK) return rc;
+    rtw_render_params q = *p;
+    q.layout = RTW_LAYOUT_IMAGE;
+    const size_t bytes = (size_t)q.width * (size_t)q.height * 3 * sizeof(float);
+    float* d = nullptr;
+    hipError_t e = hipMalloc(&d, bytes);
+    if (e != hipSuccess) {
+        rtw_world_release(g);
+        return rtw::fail(RTW_ERR_OUT_OF_MEMORY, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    // pixels outside the owned partition keep the caller's values
+    e = hipMemcpy(d, out_rgb, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        rc = rtw_render_device(g, &q, d, nullptr);
+        if (rc == RTW_OK) {
+            e = hipDeviceSynchronize();
+            if (e == hipSuccess) e = hipMemcpy(out_rgb, d, bytes, hipMemcpyDeviceToHost);
+        }
+    }
+    (void)hipFree(d);
+    rtw_world_release(g);
+    if (rc != RTW_OK) return rc;
+    if (e != hipSuccess) return rtw::fail(RTW_ERR_HIP, std::string("render: ") + hipGetErrorString(e));
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_untile_device(const rtw_render_params* p, const float* d_tiles, int64_t stride,
+                                         float* d_image, void* stream) {
+    if (!p || !d_tiles || !d_image) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    const int tw = p->tile_width > 0 ? p->tile_width : 8;
+    const int th = p->tile_height > 0 ? p->tile_height : 8;
+    const int pc = p->part_count > 0 ? p->part_count : 1;
+    const int tiles_x = (p->width + tw - 1) / tw;
+    const int n_tiles = tiles_x * ((p->height + th - 1) / th);
+    const int64_t total = (int64_t)n_tiles * tw * th;
+    if (total == 0) return RTW_OK;
+    hipLaunchKernelGGL(untile_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_tiles,
+                       stride, d_image, p->width, p->height, tw, th, tiles_x, n_tiles, pc);
+    HIP_TRY(hipGetLastError());
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_encode_rgb8_device(const float* d_image, int64_t pixels, uint8_t* d_rgb8, void* stream) {
+    if (!d_image || !d_rgb8 || pixels < 0) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
+    if (pixels == 0) return RTW_OK;
+    const int64_t n = pixels * 3;
+    hipLaunchKernelGGL(encode_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_image,
+                       pixels, d_rgb8);
+    HIP_TRY(hipGetLastError());
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_device_eval_scalar(int device, int fn, const float* a, const float* b, int64_t n, float* out) {
+    if (!a || !out || n < 0 || fn < 0 || fn > 6) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device");
+    HIP_TRY(hipSetDevice(device));
+    if (n == 0) return RTW_OK;
+    float *da = nullptr, *db = nullptr, *dout = nullptr;
+    const size_t bytes = (size_t)n * sizeof(float);
+    HIP_TRY(hipMalloc(&da, bytes));
+    HIP_TRY(hipMalloc(&db, bytes));
+    HIP_TRY(hipMalloc(&dout, bytes));
+    HIP_TRY(hipMemcpy(da, a, bytes, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(db, b ? b : a, bytes, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(eval_scalar_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, fn, da, db, n, dout);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost));
+    (void)hipFree(da);
+    (void)hipFree(db);
+    (void)hipFree(dout);
+    return RTW_OK;
+}

@@ -1,0 +1,127 @@
+"""rendering::render on the MI355X (src/lib/rendering.rs:121-252).
+
+`render` keeps the reference signature.  `thread_count` is accepted for signature parity and
+ignored: the device path has no sample split, every pixel sums all of its samples in order
+(equivalent to the reference with thread_count = 1, where merge_planes multiplies by 1.0).
+The reference seeds from entropy (rendering.rs:160); here the seed is explicit.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+from ._native import check, lib
+from .world import World
+
+
+class RenderMode(enum.IntEnum):  # rendering.rs:94-98
+    Default = N.MODE_DEFAULT
+    Normals = N.MODE_NORMALS
+
+
+@dataclass(frozen=True)
+class Size2i:  # size2i.rs:3-28
+    width: int
+    height: int
+
+    def count(self) -> int:
+        return self.width * self.height
+
+    def aspect_ratio(self) -> float:
+        return float(np.float32(self.height) / np.float32(self.width))
+
+
+DEFAULT_SEED = 0x5EED
+
+
+def render_params(
+    image_size: Size2i,
+    samples_per_pixel: int,
+    max_depth: int,
+    render_mode: RenderMode = RenderMode.Default,
+    seed: int = DEFAULT_SEED,
+    tile: tuple[int, int] = (8, 8),
+    part: tuple[int, int] = (0, 1),
+    layout: int = N.LAYOUT_IMAGE,
+) -> N.RenderParams:
+    p = N.RenderParams()
+    p.width, p.height = image_size.width, image_size.height
+    p.samples_per_pixel = samples_per_pixel
+    p.max_depth = max_depth
+    p.render_mode = int(render_mode)
+    p.layout = layout
+    p.seed = seed
+    p.tile_width, p.tile_height = tile
+    p.part_index, p.part_count = part
+    return p
+
+
+def render(
+    image_size: Size2i,
+    thread_count: int,
+    samples_per_pixel: int,
+    max_depth: int,
+    world: World,
+    render_mode: RenderMode = RenderMode.Default,
+    *,
+    seed: int = DEFAULT_SEED,
+    device: int = 0,
+) -> np.ndarray:
+    """Linear radiance, shape (H*W, 3) f32, row-major from the top-left pixel (Vec<Color>)."""
+    del thread_count
+    p = render_params(image_size, samples_per_pixel, max_depth, render_mode, seed)
+    out = np.zeros((image_size.height * image_size.width, 3), np.float32)
+    check(lib().rtw_render(world.ptr(), C.byref(p), device, out.ctypes.data_as(C.POINTER(C.c_float))))
+    return out
+
+
+class DeviceWorld:
+    """A World resident in one GPU's HBM (rtw_world_upload), rendered into torch/HIP buffers."""
+
+    def __init__(self, world: World, device: int = 0):
+        self.world = world  # keep the host tables alive
+        self.device = device
+        h = C.c_void_p()
+        check(lib().rtw_world_upload(world.ptr(), device, C.byref(h)))
+        self._h = h
+
+    def release(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().rtw_world_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+    def render_into(self, params: N.RenderParams, d_out_ptr: int, stream_ptr: int | None = None) -> None:
+        """Asynchronous launch on `stream_ptr` (hipStream_t) into device pointer `d_out_ptr`."""
+        check(lib().rtw_render_device(self._h, C.byref(params), C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr or 0)))
+
+    def collect_stats(self, params: N.RenderParams) -> dict:
+        s = N.RenderStats()
+        check(lib().rtw_render_collect_stats(self._h, C.byref(params), C.byref(s)))
+        return s.as_dict()
+
+
+def partition_floats(params: N.RenderParams) -> int:
+    n = C.c_int64()
+    check(lib().rtw_partition_floats(C.byref(params), C.byref(n)))
+    return n.value
+
+
+def untile_device(params: N.RenderParams, d_tiles: int, stride_floats: int, d_image: int, stream_ptr: int | None = None):
+    check(lib().rtw_untile_device(C.byref(params), C.c_void_p(d_tiles), stride_floats, C.c_void_p(d_image),
+                                  C.c_void_p(stream_ptr or 0)))
+
+
+def device_count() -> int:
+    n = C.c_int()
+    check(lib().rtw_device_count(C.byref(n)))
+    return n.value
