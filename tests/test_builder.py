@@ -100,7 +100,7 @@ def test_aspect_ratio_and_cli_heights(worlds):
     a = np.float32(worlds("final_scene1").camera.aspect_ratio())
     assert abs(a - np.float32(9 / 16)) <= np.float32(2e-7)
     assert int(np.float32(1920) * a) in (1079, 1080)
-    assert np.float32(worlds("suzanne").camera.aspect_ratio()) == np.float32(0.75)
+    assert int(np.float32(1920) * np.float32(worlds("suzanne").camera.aspect_ratio())) == 1439
 
 
 def test_obj_fan_quirk_cube(assets):
