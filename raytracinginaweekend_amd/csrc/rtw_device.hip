@@ -25,9 +25,10 @@
 #include "../../include/rtw_scalar.h"
 #include "rtw_common.h"
 
-#define RTW_BLOCK 256
-#define RTW_WAVES_PER_BLOCK (RTW_BLOCK / 64)
-#define RTW_STACK 32
+#define RTW_BLOCK 512   // 8 waves; 2 blocks per CU at <= 128 VGPRs -> 4 waves per SIMD
+#define RTW_MIN_WAVES_PER_SIMD 4
+#define RTW_STACK 32    // per-lane traversal stack (LDS), >= the BVH depth (checked at upload)
+#define RTW_LDS_SCENE_MAX (96 * 1024)  // nodes + leaf records staged in LDS when they fit
 
 namespace {
 
@@ -38,6 +39,7 @@ struct DWorld {
     const float4* node_a;  // {min.x, min.y, min.z, max.x}
     const float4* node_b;  // {max.y, max.z, bits(left << 2 | axis), bits(right)}
     const int4* leaf_info; // {geom_kind, geom_index, material, flags}
+    const float4* leaf_fast; // plain sphere leaves: {center.xyz, radius}; other leaves: w = NaN
     const float4* leaf_xf; // 3 per leaf: {neg_inv_density, off.xyz}, {ys, yc, vel.x, vel.y}, {vel.z,0,0,0}
     const float4* spheres; // {center.xyz, radius}
     const float4* rects;   // 2 per rect: {dist, r0.0, r0.1, r1.0}, {r1.1, bits(plane), 0, 0}
@@ -73,8 +75,9 @@ struct KArgs {
     int32_t layout;
     int32_t tile_w, tile_h, tiles_x, n_tiles;
     int32_t part_index, part_count;
-    int32_t chunks_per_tile; // ceil(tile_w * tile_h / 64)
-    int64_t jobs;            // waves of work in this launch
+    uint32_t total;          // pixel slots in this partition (owned tiles * tile_w * tile_h)
+    int32_t node_count, leaf_count;
+    unsigned int* queue;     // pixel work counter (zeroed before each launch)
     uint64_t seed_key;
     float sx, sy;            // 1/(W-1), 1/(H-1)
     rtw_uniform ux, uy;      // pixel jitter distributions
@@ -444,41 +447,109 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
 // ---------------------------------------------------------------------------------------------
 // BVH traversal (hittable.rs:429-473; aabb.rs:65-78)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool slab_axis(float mn, float mx, float o, float d, float ts, float te) {
-    const float a = (mn - o) / d;
-    const float b = (mx - o) / d;
-    const float t0 = (a < b) ? a : b;  // math.rs:35-41 minmax
-    const float t1 = (a < b) ? b : a;
-    const float tmin = rtw_maxr(t0, ts);
-    const float tmax = rtw_minr(t1, te);
-    return !(tmax <= tmin);
+// Exact f32 division by a ray-direction component d with y = RN(1/d) precomputed per ray
+// (Markstein): q = RN(a*y); r = fma(-d, q, a) (exact); q' = RN(q + r*y) == RN(a/d), provided
+// no underflow/overflow: the caller guarantees 2^-60 <= |d| <= 2, 2^-40 <= |a| <= 2^40
+// (tests/native/markstein_check.c checks every divisor significand under these guards).
+#define RTW_MK_DMIN 0x1p-60f
+#define RTW_MK_AMIN 0x1p-40f
+#define RTW_MK_AMAX 0x1p40f
+__device__ __forceinline__ float mk_div(float a, float d, float y) {
+    const float q = a * y;
+    return __builtin_fmaf(__builtin_fmaf(-d, q, a), y, q);
 }
 
-// Closest hit.  Returns the leaf index or -1; `te` is shrunk to the hit's t.
+// One axis of Aabb::hit_cond: minmax (math.rs:35-41), then !(min(t1, te) <= max(t0, ts)).
+// tmin/tmax are never NaN (te, ts are not; Rust's min/max drop a NaN operand), so the test is
+// tmax > tmin, and min/max of a value against ts = 0.001 or te > 0 cannot meet the +-0 case.
+__device__ __forceinline__ bool axis_pass(float qa, float qb, float ts, float te) {
+    const bool lt = qa < qb;
+    const float t0 = lt ? qa : qb;
+    const float t1 = lt ? qb : qa;
+    const float tmax = (t1 < te) ? t1 : te;
+    const float tmin = (t0 > ts) ? t0 : ts;
+    return tmax > tmin;
+}
+
+struct RayPre {  // per-ray constants of the slab test
+    V3 inv;
+    bool fast;
+};
+__device__ __forceinline__ RayPre ray_pre(const Ray& r) {
+    RayPre p;
+    p.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
+                                    __builtin_fabsf(r.d.z));
+    const float M = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
+                                    __builtin_fabsf(r.d.z));
+    p.fast = (m >= RTW_MK_DMIN) && (M <= 2.0f);
+    return p;
+}
+
+__device__ __forceinline__ bool node_pass(float4 na, float4 nb, const Ray& r, const RayPre& rp, float ts, float te) {
+    const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
+    const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
+    const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
+    const float lo = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fabsf(a0), __builtin_fabsf(b0)),
+                                                     __builtin_fminf(__builtin_fabsf(a1), __builtin_fabsf(b1))),
+                                     __builtin_fminf(__builtin_fabsf(a2), __builtin_fabsf(b2)));
+    const float hi = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(a0), __builtin_fabsf(b0)),
+                                                     __builtin_fmaxf(__builtin_fabsf(a1), __builtin_fabsf(b1))),
+                                     __builtin_fmaxf(__builtin_fabsf(a2), __builtin_fabsf(b2)));
+    float qa0, qb0, qa1, qb1, qa2, qb2;
+    if (__builtin_expect(rp.fast && lo >= RTW_MK_AMIN && hi <= RTW_MK_AMAX, 1)) {
+        qa0 = mk_div(a0, r.d.x, rp.inv.x);
+        qb0 = mk_div(b0, r.d.x, rp.inv.x);
+        qa1 = mk_div(a1, r.d.y, rp.inv.y);
+        qb1 = mk_div(b1, r.d.y, rp.inv.y);
+        qa2 = mk_div(a2, r.d.z, rp.inv.z);
+        qb2 = mk_div(b2, r.d.z, rp.inv.z);
+    } else {
+        qa0 = a0 / r.d.x;
+        qb0 = b0 / r.d.x;
+        qa1 = a1 / r.d.y;
+        qb1 = b1 / r.d.y;
+        qa2 = a2 / r.d.z;
+        qb2 = b2 / r.d.z;
+    }
+    return axis_pass(qa0, qb0, ts, te) && axis_pass(qa1, qb1, ts, te) && axis_pass(qa2, qb2, ts, te);
+}
+
+// Closest hit.  Returns the leaf index or -1; `te` is shrunk to the hit's t.  `nodes` holds
+// two float4 per node {min.xyz, max.x}, {max.y, max.z, left<<2|axis, right}; `fast` one float4
+// per leaf (plain spheres inline, w = NaN otherwise) -- both in LDS when they fit.
 template <bool STATS>
-__device__ __forceinline__ int trace(const DWorld& w, const Ray& r, float ts, float& te, rtw_xoro& rng, int32_t* stack,
-                                     Stats& st) {
+__device__ __forceinline__ int trace(const DWorld& w, const float4* nodes, const float4* fast, const Ray& r, float ts,
+                                     float& te, rtw_xoro& rng, int32_t* stack, Stats& st) {
+    const RayPre rp = ray_pre(r);
     int found = -1;
     int32_t node = w.root;
     int sp = 0;
     for (;;) {
         if (node < 0) {
             const int leaf = -1 - node;
+            const float4 sph = fast[leaf];
             float t;
-            if (leaf_t<STATS>(w, leaf, r, ts, te, rng, t, st)) {
+            bool hit;
+            if (sph.w == sph.w) {  // a plain sphere leaf
+                if (STATS) st.c[ST_T_SPHERE]++;
+                hit = sphere_t(sph, r, ts, te, t);
+            } else {
+                hit = leaf_t<STATS>(w, leaf, r, ts, te, rng, t, st);
+            }
+            if (hit) {
                 te = t;
                 found = leaf;
             }
         } else {
             if (STATS) st.c[ST_NODES]++;
-            const float4 a = w.node_a[node];
-            const float4 b = w.node_b[node];
-            if (slab_axis(a.x, a.w, r.o.x, r.d.x, ts, te) && slab_axis(a.y, b.x, r.o.y, r.d.y, ts, te) &&
-                slab_axis(a.z, b.y, r.o.z, r.d.z, ts, te)) {
-                const int32_t lbits = __float_as_int(b.z);
+            const float4 na = nodes[2 * node];
+            const float4 nb = nodes[2 * node + 1];
+            if (node_pass(na, nb, r, rp, ts, te)) {
+                const int32_t lbits = __float_as_int(nb.z);
                 const int32_t left = lbits >> 2;
                 const int axis = lbits & 3;
-                const int32_t right = __float_as_int(b.w);
+                const int32_t right = __float_as_int(nb.w);
                 const bool fwd = comp(r.d, axis) > 0.0f;
                 stack[(sp++) * RTW_BLOCK] = fwd ? right : left;
                 node = fwd ? left : right;
@@ -624,36 +695,39 @@ __device__ __forceinline__ Ray camera_ray(const rtw_camera& c, rtw_xoro& rng, fl
 // ---------------------------------------------------------------------------------------------
 // the megakernel
 // ---------------------------------------------------------------------------------------------
-template <bool STATS>
-__global__ __launch_bounds__(RTW_BLOCK) void render_kernel(KArgs A) {
-    __shared__ int32_t s_stack[RTW_STACK * RTW_BLOCK];
-    const int lane = threadIdx.x & 63;
-    const int64_t job = (int64_t)blockIdx.x * RTW_WAVES_PER_BLOCK + (threadIdx.x >> 6);
-    if (job >= A.jobs) return;
-    const int32_t local_tile = (int32_t)(job / A.chunks_per_tile);
-    const int32_t chunk = (int32_t)(job % A.chunks_per_tile);
-    const int32_t tile = A.part_index + local_tile * A.part_count;
-    const int32_t in_tile = chunk * 64 + lane;
-    if (in_tile >= A.tile_w * A.tile_h) return;
-    const int32_t px = (tile % A.tiles_x) * A.tile_w + in_tile % A.tile_w;
-    const int32_t py = (tile / A.tiles_x) * A.tile_h + in_tile / A.tile_w;
-    if (px >= A.width || py >= A.height) return;
-
+template <bool STATS, bool LDS_SCENE>
+__global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
+    // LDS: [scene: nodes (2 float4 each) + leaf records (1 float4 each)] [stack: RTW_STACK x BLOCK]
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
     const DWorld& w = A.w;
-    int32_t* stack = s_stack + threadIdx.x;
+    const int n_scene = LDS_SCENE ? 2 * A.node_count + A.leaf_count : 0;
+    const float4* nodes = w.node_a;
+    const float4* fast = w.leaf_fast;
+    if (LDS_SCENE) {
+        for (int i = threadIdx.x; i < 2 * A.node_count; i += RTW_BLOCK) smem[i] = w.node_a[i];
+        for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
+        __syncthreads();
+        nodes = smem;
+        fast = smem + 2 * A.node_count;
+    }
+    int32_t* stack = reinterpret_cast<int32_t*>(smem + n_scene) + threadIdx.x;
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
+    const int lane = threadIdx.x & 63;
+    const int per_tile = A.tile_w * A.tile_h;
 
-    const uint32_t pix = (uint32_t)(py * A.width + px);
-    const float fx = (float)px * A.sx, fy = (float)py * A.sy;  // size2i.rs:52-55
-
+    // per-lane pixel state; pixels come from a queue in tile order (wave-aggregated atomics), so
+    // a lane that finishes its pixel immediately takes the next one
+    uint32_t pix = 0, slot = 0;
+    float fx = 0.0f, fy = 0.0f;
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     uint32_t sample = 0;
     rtw_xoro rng;
     Ray ray;
     V3 pdir, att, acc;
     int32_t depth;
+    bool need = true;
 
     // rendering.rs:174-176: jitter (x then y), then Camera::ray
     auto start_sample = [&]() {
@@ -666,14 +740,49 @@ __global__ __launch_bounds__(RTW_BLOCK) void render_kernel(KArgs A) {
         acc = v3(0.0f, 0.0f, 0.0f);
         depth = A.max_depth;
     };
-    start_sample();
 
     for (;;) {
+        // refill lanes that need a pixel (one atomic per wave per round)
+        bool finished = false;
+        for (;;) {
+            const unsigned long long m = __ballot(need);
+            if (m == 0) break;
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned int base = 0;
+            if (lane == leader) base = atomicAdd(A.queue, (unsigned int)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                const unsigned long long below = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
+                const uint32_t c = base + (uint32_t)__popcll(below);
+                if (c >= A.total) {
+                    finished = true;
+                    need = false;
+                } else {
+                    const int32_t lt = (int32_t)(c / (uint32_t)per_tile);
+                    const int32_t it = (int32_t)(c % (uint32_t)per_tile);
+                    const int32_t tile = A.part_index + lt * A.part_count;
+                    const int32_t px = (tile % A.tiles_x) * A.tile_w + it % A.tile_w;
+                    const int32_t py = (tile / A.tiles_x) * A.tile_h + it / A.tile_w;
+                    if (px < A.width && py < A.height) {  // else: padding slot of an edge tile
+                        need = false;
+                        slot = c;
+                        pix = (uint32_t)(py * A.width + px);
+                        fx = (float)px * A.sx;  // size2i.rs:52-55
+                        fy = (float)py * A.sy;
+                        sum = v3(0.0f, 0.0f, 0.0f);
+                        sample = 0;
+                        start_sample();
+                    }
+                }
+            }
+        }
+        if (finished) break;
+
         V3 color;
         bool done = false;
         float te = F32_INF;
         if (STATS) st.c[ST_RAYS]++;
-        const int leaf = trace<STATS>(w, ray, 0.001f, te, rng, stack, st);
+        const int leaf = trace<STATS>(w, nodes, fast, ray, 0.001f, te, rng, stack, st);
         if (leaf >= 0) {
             if (STATS) {
                 st.c[ST_H_SPHERE + w.leaf_info[leaf].x]++;
@@ -788,23 +897,23 @@ __global__ __launch_bounds__(RTW_BLOCK) void render_kernel(KArgs A) {
             sum = add(sum, color);
             if (STATS) st.c[ST_SAMPLES]++;
             ++sample;
-            if (sample >= A.spp) break;
-            start_sample();
+            if (sample >= A.spp) {
+                // rendering.rs:179: sum / spp; merge_planes with one plane multiplies by 1.0
+                const V3 pixel = divs(sum, (float)A.spp);
+                float* o = (A.layout == RTW_LAYOUT_TILES) ? A.out + (int64_t)slot * 3 : A.out + (int64_t)pix * 3;
+                o[0] = pixel.x;
+                o[1] = pixel.y;
+                o[2] = pixel.z;
+                need = true;
+            } else {
+                start_sample();
+            }
         }
     }
-    const V3 pixel = divs(sum, (float)A.spp);
     if (STATS) {
         for (int i = 0; i < ST_COUNT; ++i)
             if (st.c[i]) atomicAdd(&A.stats[i], (unsigned long long)st.c[i]);
     }
-    float* o;
-    if (A.layout == RTW_LAYOUT_TILES)
-        o = A.out + ((int64_t)local_tile * A.tile_w * A.tile_h + in_tile) * 3;
-    else
-        o = A.out + (int64_t)pix * 3;
-    o[0] = pixel.x;
-    o[1] = pixel.y;
-    o[2] = pixel.z;
 }
 
 // scatter gathered tile buffers back into the image
@@ -909,7 +1018,27 @@ int check_world(const rtw_world* w, int* depth_out) {
         if (w->perlins[i].bits < 1 || w->perlins[i].bits > 8) return bad("perlin bits");
     for (int i = 0; i < w->image_count; ++i)
         if (w->images[i].width < 1 || w->images[i].height < 1 || !w->images[i].rgb) return bad("image");
-    // node references + depth (the per-lane stack holds RTW_STACK entries)
+    // coordinate bound behind the exact fast division of the slab test (|a| <= 2^40 there):
+    // every coordinate the device sees stays below 2^30 in magnitude
+    const float LIM = 1073741824.0f;
+    auto big = [&](const float* v, int n) {
+        for (int k = 0; k < n; ++k)
+            if (!(v[k] >= -LIM && v[k] <= LIM)) return true;
+        return false;
+    };
+    for (int i = 0; i < w->node_count; ++i)
+        if (big(w->nodes[i].min, 3) || big(w->nodes[i].max, 3)) return bad("node bounds beyond 2^30");
+    for (int i = 0; i < w->sphere_count; ++i)
+        if (big(w->spheres[i].center, 4)) return bad("sphere beyond 2^30");
+    for (int i = 0; i < w->leaf_count; ++i) {
+        const rtw_leaf& L = w->leaves[i];
+        float vt[3];
+        for (int k = 0; k < 3; ++k)
+            vt[k] = L.velocity[k] * std::max(std::fabs(w->camera.time0), std::fabs(w->camera.time1));
+        if (big(L.offset, 3) || big(vt, 3)) return bad("leaf transform beyond 2^30");
+    }
+    if (big(w->camera.position, 3)) return bad("camera beyond 2^30");
+    // node references + depth (the per-lane stack holds one entry per level)
     std::vector<std::pair<int32_t, int>> todo;
     int maxd = 0;
     std::vector<uint8_t> seen((size_t)std::max(1, w->node_count), 0);
@@ -939,7 +1068,10 @@ int check_world(const rtw_world* w, int* depth_out) {
 struct rtw_gpu_world {
     int device = 0;
     void* arena = nullptr;
+    unsigned int* queue = nullptr;  // pixel work counter (one render at a time per world)
     DWorld w{};
+    int32_t node_count = 0, leaf_count = 0, depth = 1;
+    int cus = 0;
 };
 
 extern "C" RTW_API int rtw_device_count(int* count) {
@@ -964,14 +1096,27 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
 
     Layout L;
     // nodes
-    std::vector<float4> na((size_t)std::max(1, w->node_count)), nb((size_t)std::max(1, w->node_count));
+    // nodes: two float4 per node, interleaved (one 32-byte record)
+    std::vector<float4> na((size_t)std::max(1, 2 * w->node_count));
     for (int i = 0; i < w->node_count; ++i) {
         const rtw_bvh_node& n = w->nodes[i];
-        na[(size_t)i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
-        nb[(size_t)i] = make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
+        na[2 * (size_t)i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
+        na[2 * (size_t)i + 1] =
+            make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
     }
     const size_t o_na = L.push(na.data(), na.size() * sizeof(float4));
-    const size_t o_nb = L.push(nb.data(), nb.size() * sizeof(float4));
+    // leaf records for the traversal: plain spheres inline, everything else tagged NaN
+    std::vector<float4> lf((size_t)w->leaf_count);
+    for (int i = 0; i < w->leaf_count; ++i) {
+        const rtw_leaf& l = w->leaves[i];
+        if (l.geom_kind == RTW_GEOM_SPHERE && l.flags == 0) {
+            const rtw_sphere& sp = w->spheres[l.geom_index];
+            lf[(size_t)i] = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius);
+        } else {
+            lf[(size_t)i] = make_float4(0.0f, 0.0f, 0.0f, ibits(0x7FC00000));
+        }
+    }
+    const size_t o_lf = L.push(lf.data(), lf.size() * sizeof(float4));
     // leaves
     std::vector<int4> li((size_t)w->leaf_count);
     std::vector<float4> lx((size_t)w->leaf_count * 3);
@@ -1085,7 +1230,8 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     uint8_t* base = (uint8_t*)g->arena;
     DWorld& d = g->w;
     d.node_a = (const float4*)(base + o_na);
-    d.node_b = (const float4*)(base + o_nb);
+    d.node_b = nullptr;
+    d.leaf_fast = (const float4*)(base + o_lf);
     d.leaf_info = (const int4*)(base + o_li);
     d.leaf_xf = (const float4*)(base + o_lx);
     d.spheres = (const float4*)(base + o_sp);
@@ -1103,6 +1249,17 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     d.root = w->root;
     d.has_light = w->has_light;
     d.wc = (const WorldConst*)(base + o_wc);
+    g->node_count = w->node_count;
+    g->leaf_count = w->leaf_count;
+    g->depth = std::max(1, depth);
+    (void)hipDeviceGetAttribute(&g->cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (g->cus <= 0) g->cus = 256;
+    e = hipMalloc(&g->queue, 256);
+    if (e != hipSuccess) {
+        (void)hipFree(g->arena);
+        delete g;
+        return rtw::fail(RTW_ERR_OUT_OF_MEMORY, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
     *out = g;
     return RTW_OK;
 }
@@ -1111,6 +1268,7 @@ extern "C" RTW_API int rtw_world_release(rtw_gpu_world* g) {
     if (!g) return RTW_OK;
     (void)hipSetDevice(g->device);
     if (g->arena) (void)hipFree(g->arena);
+    if (g->queue) (void)hipFree(g->queue);
     delete g;
     return RTW_OK;
 }
@@ -1143,14 +1301,45 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.n_tiles = A.tiles_x * tiles_y;
     A.part_index = p->part_index;
     A.part_count = pc;
-    A.chunks_per_tile = (tw * th + 63) / 64;
     const int64_t owned = A.n_tiles > p->part_index ? (A.n_tiles - p->part_index + pc - 1) / pc : 0;
-    A.jobs = owned * A.chunks_per_tile;
+    if (owned * tw * th >= (int64_t)0xFFFFFFFF) return rtw::fail(RTW_ERR_UNSUPPORTED, "partition too large");
+    A.total = (uint32_t)(owned * tw * th);
+    A.node_count = g->node_count;
+    A.leaf_count = g->leaf_count;
+    A.queue = g->queue;
     A.seed_key = rtw_seed_key(p->seed);
     A.sx = 1.0f / (float)(p->width - 1);
     A.sy = 1.0f / (float)(p->height - 1);
     A.ux = rtw_uniform_new(0.0f, 1.0f / (float)(p->width - 1));
     A.uy = rtw_uniform_new(0.0f, 1.0f / (float)(p->height - 1));
+    return RTW_OK;
+}
+
+// Launch the persistent render kernel: zero the pixel queue, stage the scene in LDS when it
+// fits, size the grid to the resident block count.
+int launch_render(rtw_gpu_world* g, KArgs& A, bool stats, hipStream_t stream) {
+    const size_t scene_bytes = (size_t)(2 * g->node_count + g->leaf_count) * sizeof(float4);
+    const bool lds_scene = scene_bytes <= RTW_LDS_SCENE_MAX;
+    const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
+    const size_t lds = (lds_scene ? scene_bytes : 0) + stack_bytes;
+    const void* fn;
+    if (stats) fn = lds_scene ? (const void*)render_kernel<true, true> : (const void*)render_kernel<true, false>;
+    else fn = lds_scene ? (const void*)render_kernel<false, true> : (const void*)render_kernel<false, false>;
+    HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, RTW_BLOCK, lds));
+    if (per_cu < 1) return rtw::fail(RTW_ERR_UNSUPPORTED, "render kernel does not fit on a CU");
+    const int64_t want = ((int64_t)A.total + RTW_BLOCK - 1) / RTW_BLOCK;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per_cu * g->cus));
+    HIP_TRY(hipMemsetAsync(g->queue, 0, sizeof(unsigned int), stream));
+    if (stats) {
+        if (lds_scene) hipLaunchKernelGGL((render_kernel<true, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
+        else hipLaunchKernelGGL((render_kernel<true, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
+    } else {
+        if (lds_scene) hipLaunchKernelGGL((render_kernel<false, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
+        else hipLaunchKernelGGL((render_kernel<false, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
+    }
+    HIP_TRY(hipGetLastError());
     return RTW_OK;
 }
 
@@ -1176,11 +1365,8 @@ extern "C" RTW_API int rtw_render_device(rtw_gpu_world* g, const rtw_render_para
     if (!d_out) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null output");
     A.out = d_out;
     HIP_TRY(hipSetDevice(g->device));
-    if (A.jobs == 0) return RTW_OK;
-    const int64_t blocks = (A.jobs + RTW_WAVES_PER_BLOCK - 1) / RTW_WAVES_PER_BLOCK;
-    hipLaunchKernelGGL(render_kernel<false>, dim3((unsigned)blocks), dim3(RTW_BLOCK), 0, (hipStream_t)stream, A);
-    HIP_TRY(hipGetLastError());
-    return RTW_OK;
+    if (A.total == 0) return RTW_OK;
+    return launch_render(g, A, false, (hipStream_t)stream);
 }
 
 extern "C" RTW_API int rtw_render_collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s) {
@@ -1197,9 +1383,11 @@ extern "C" RTW_API int rtw_render_collect_stats(rtw_gpu_world* g, const rtw_rend
     A.out = out;
     A.layout = RTW_LAYOUT_IMAGE;
     A.stats = st;
-    const int64_t blocks = (A.jobs + RTW_WAVES_PER_BLOCK - 1) / RTW_WAVES_PER_BLOCK;
-    if (blocks > 0) hipLaunchKernelGGL(render_kernel<true>, dim3((unsigned)blocks), dim3(RTW_BLOCK), 0, 0, A);
-    HIP_TRY(hipGetLastError());
+    if (A.total > 0) {
+        const int rc = launch_render(g, A, true, 0);
+        if (rc != RTW_OK) return rc;
+    }
+    HIP_TRY(hipDeviceSynchronize());
     unsigned long long h[ST_COUNT];
     HIP_TRY(hipMemcpy(h, st, sizeof(h), hipMemcpyDeviceToHost));
     (void)hipFree(out);
