@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -78,6 +79,8 @@ struct KArgs {
     uint32_t total;          // pixel slots in this partition (owned tiles * tile_w * tile_h)
     int32_t node_count, leaf_count;
     unsigned int* queue;     // pixel work counter (zeroed before each launch)
+    int32_t trace_min;       // dynamic ray fetch threshold (lanes still tracing)
+    const DWorld* wdev;      // a copy of `w` in device memory (for the out-of-line shader)
     uint64_t seed_key;
     float sx, sy;            // 1/(W-1), 1/(H-1)
     rtw_uniform ux, uy;      // pixel jitter distributions
@@ -695,108 +698,46 @@ __device__ __forceinline__ Ray camera_ray(const rtw_camera& c, rtw_xoro& rng, fl
 // ---------------------------------------------------------------------------------------------
 // the megakernel
 // ---------------------------------------------------------------------------------------------
-template <bool STATS, bool LDS_SCENE>
-__global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
-    // LDS: [scene: nodes (2 float4 each) + leaf records (1 float4 each)] [stack: RTW_STACK x BLOCK]
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    const DWorld& w = A.w;
-    const int n_scene = LDS_SCENE ? 2 * A.node_count + A.leaf_count : 0;
-    const float4* nodes = w.node_a;
-    const float4* fast = w.leaf_fast;
-    if (LDS_SCENE) {
-        for (int i = threadIdx.x; i < 2 * A.node_count; i += RTW_BLOCK) smem[i] = w.node_a[i];
-        for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
-        __syncthreads();
-        nodes = smem;
-        fast = smem + 2 * A.node_count;
-    }
-    int32_t* stack = reinterpret_cast<int32_t*>(smem + n_scene) + threadIdx.x;
-    Stats st;
-    if (STATS)
-        for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
-    const int lane = threadIdx.x & 63;
-    const int per_tile = A.tile_w * A.tile_h;
-
-    // per-lane pixel state; pixels come from a queue in tile order (wave-aggregated atomics), so
-    // a lane that finishes its pixel immediately takes the next one
-    uint32_t pix = 0, slot = 0;
-    float fx = 0.0f, fy = 0.0f;
-    V3 sum = v3(0.0f, 0.0f, 0.0f);
-    uint32_t sample = 0;
-    rtw_xoro rng;
+// ---------------------------------------------------------------------------------------------
+// shading: one bounce of ray_color (rendering.rs:19-71), out of line so that its temporaries
+// and hoisted invariants never pressure the traversal loop's registers
+// ---------------------------------------------------------------------------------------------
+struct Path {  // per-path state crossing the call by value (registers)
     Ray ray;
-    V3 pdir, att, acc;
+    V3 att, acc;
     int32_t depth;
-    bool need = true;
+    rtw_xoro rng;
+};
+struct ShadeOut {
+    Path p;
+    V3 color;
+    int32_t done;   // 1: the sample is finished, `color` is its radiance
+    uint32_t texels;
+};
 
-    // rendering.rs:174-176: jitter (x then y), then Camera::ray
-    auto start_sample = [&]() {
-        rng = rtw_sample_stream(A.seed_key, pix, sample);
-        const float jx = rtw_uniform_sample(&A.ux, &rng);
-        const float jy = rtw_uniform_sample(&A.uy, &rng);
-        ray = camera_ray(w.wc->cam, rng, fx + jx, fy + jy);
-        pdir = ray.d;
-        att = v3(1.0f, 1.0f, 1.0f);
-        acc = v3(0.0f, 0.0f, 0.0f);
-        depth = A.max_depth;
-    };
-
-    for (;;) {
-        // refill lanes that need a pixel (one atomic per wave per round)
-        bool finished = false;
-        for (;;) {
-            const unsigned long long m = __ballot(need);
-            if (m == 0) break;
-            const int leader = __ffsll((long long)m) - 1;
-            unsigned int base = 0;
-            if (lane == leader) base = atomicAdd(A.queue, (unsigned int)__popcll(m));
-            base = __shfl(base, leader);
-            if (need) {
-                const unsigned long long below = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
-                const uint32_t c = base + (uint32_t)__popcll(below);
-                if (c >= A.total) {
-                    finished = true;
-                    need = false;
-                } else {
-                    const int32_t lt = (int32_t)(c / (uint32_t)per_tile);
-                    const int32_t it = (int32_t)(c % (uint32_t)per_tile);
-                    const int32_t tile = A.part_index + lt * A.part_count;
-                    const int32_t px = (tile % A.tiles_x) * A.tile_w + it % A.tile_w;
-                    const int32_t py = (tile / A.tiles_x) * A.tile_h + it / A.tile_w;
-                    if (px < A.width && py < A.height) {  // else: padding slot of an edge tile
-                        need = false;
-                        slot = c;
-                        pix = (uint32_t)(py * A.width + px);
-                        fx = (float)px * A.sx;  // size2i.rs:52-55
-                        fy = (float)py * A.sy;
-                        sum = v3(0.0f, 0.0f, 0.0f);
-                        sample = 0;
-                        start_sample();
-                    }
-                }
-            }
-        }
-        if (finished) break;
-
-        V3 color;
-        bool done = false;
-        float te = F32_INF;
-        if (STATS) st.c[ST_RAYS]++;
-        const int leaf = trace<STATS>(w, nodes, fast, ray, 0.001f, te, rng, stack, st);
-        if (leaf >= 0) {
-            if (STATS) {
-                st.c[ST_H_SPHERE + w.leaf_info[leaf].x]++;
-                st.c[ST_MAT]++;
-            }
-            Hit h;
-            leaf_record(w, leaf, ray, te, h);
-            if (A.mode == RTW_MODE_NORMALS) {  // rendering.rs:110-113
-                color = mul(add(h.n, v3(1.0f, 1.0f, 1.0f)), 0.5f);
-                done = true;
-            } else if (depth <= 1) {  // rendering.rs:26-27
-                color = v3(0.0f, 0.0f, 0.0f);
-                done = true;
-            } else {
+template <bool STATS>
+__device__ __noinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t mode, Path P, int32_t found, float te,
+                                       V3 pdir) {
+    const DWorld& w = *wp;
+    Stats st;
+    st.c[ST_TEXEL] = 0;
+    Ray& ray = P.ray;
+    V3& att = P.att;
+    V3& acc = P.acc;
+    int32_t& depth = P.depth;
+    rtw_xoro& rng = P.rng;
+    V3 color = v3(0.0f, 0.0f, 0.0f);
+    bool done = false;
+    if (found >= 0) {
+        Hit h;
+        leaf_record(w, found, ray, te, h);
+        if (mode == RTW_MODE_NORMALS) {  // rendering.rs:110-113
+            color = mul(add(h.n, v3(1.0f, 1.0f, 1.0f)), 0.5f);
+            done = true;
+        } else if (depth <= 1) {  // rendering.rs:26-27
+            color = v3(0.0f, 0.0f, 0.0f);
+            done = true;
+        } else {
                 const int4 M = w.materials[h.material];
                 const int mkind = M.x;
                 // Material::scatter (material.rs:52-114).  At most one texture lookup per bounce:
@@ -887,26 +828,249 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
                     color = add(acc, conv(att, emitted));
                     done = true;
                 }
-            }
-        } else {
-            // rendering.rs:67 (background of the PRIMARY ray) / :114
-            color = add(acc, conv(att, background(w.wc->bg, pdir)));
-            done = true;
         }
-        if (done) {
-            sum = add(sum, color);
-            if (STATS) st.c[ST_SAMPLES]++;
-            ++sample;
-            if (sample >= A.spp) {
-                // rendering.rs:179: sum / spp; merge_planes with one plane multiplies by 1.0
-                const V3 pixel = divs(sum, (float)A.spp);
-                float* o = (A.layout == RTW_LAYOUT_TILES) ? A.out + (int64_t)slot * 3 : A.out + (int64_t)pix * 3;
-                o[0] = pixel.x;
-                o[1] = pixel.y;
-                o[2] = pixel.z;
-                need = true;
+    } else {
+        // rendering.rs:67 (background of the PRIMARY ray) / :114
+        color = add(acc, conv(att, background(w.wc->bg, pdir)));
+        done = true;
+    }
+    ShadeOut o;
+    o.p = P;
+    o.color = color;
+    o.done = done ? 1 : 0;
+    o.texels = STATS ? st.c[ST_TEXEL] : 0u;
+    return o;
+}
+
+enum { PH_PIXEL = 0, PH_TRACE = 1, PH_SHADE = 2 };
+
+extern __shared__ __attribute__((aligned(16))) float4 smem[];
+
+// Traversal state of one lane (by value, in registers, across the out-of-line call).
+struct Trav {
+    Ray ray;
+    V3 inv;         // RN(1 / ray.d)
+    int32_t fast;   // Markstein division usable for this ray
+    int32_t node;   // current node (>= 0) or ~leaf
+    int32_t sp;
+    float te;       // t_range.end, shrunk by every hit (hittable.rs:457)
+    int32_t found;  // closest leaf so far, -1 if none
+    rtw_xoro rng;   // volumes draw from the path's stream during traversal
+    int32_t phase;
+    // statistics of one call (counting variant); tests packed 16 bits per kind (a lane traces at
+    // most one ray's remainder per call: far below 2^16 tests of one kind)
+    uint32_t n_nodes, n_sph_rect, n_box_tri;
+};
+
+// The hot loop: every lane in PH_TRACE advances one node or leaf per iteration until fewer than
+// `trace_min` lanes are still tracing while some lane waits for shading (dynamic ray fetch).
+// Out of line so that it gets a register allocation of its own.
+template <bool STATS, bool LDS_SCENE>
+__device__ __noinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
+                                      int32_t n_leaves) {
+    const DWorld& w = *wp;
+    const float4* nodes = LDS_SCENE ? smem : w.node_a;
+    const float4* fast = LDS_SCENE ? smem + 2 * n_nodes : w.leaf_fast;
+    int32_t* stack = reinterpret_cast<int32_t*>(smem + (LDS_SCENE ? 2 * n_nodes + n_leaves : 0)) + threadIdx.x;
+    Stats st;
+    if (STATS)
+        for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
+    const RayPre rp{T.inv, T.fast != 0};
+    for (;;) {
+        const unsigned long long tr = __ballot(T.phase == PH_TRACE);
+        if (tr == 0) break;
+        if (__popcll(tr) < (unsigned)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
+        if (T.phase == PH_TRACE) {
+            bool descended = false;
+            if (T.node >= 0) {
+                if (STATS) st.c[ST_NODES]++;
+                const float4 na = nodes[2 * T.node];
+                const float4 nb = nodes[2 * T.node + 1];
+                if (node_pass(na, nb, T.ray, rp, 0.001f, T.te)) {
+                    const int32_t lbits = __float_as_int(nb.z);
+                    const int32_t left = lbits >> 2;
+                    const int axis = lbits & 3;
+                    const int32_t right = __float_as_int(nb.w);
+                    const bool fwd = comp(T.ray.d, axis) > 0.0f;
+                    stack[(T.sp++) * RTW_BLOCK] = fwd ? right : left;
+                    T.node = fwd ? left : right;
+                    descended = true;
+                }
             } else {
-                start_sample();
+                const int leaf = -1 - T.node;
+                const float4 sph = fast[leaf];
+                float t;
+                bool hit;
+                if (sph.w == sph.w) {  // a plain sphere leaf
+                    if (STATS) st.c[ST_T_SPHERE]++;
+                    hit = sphere_t(sph, T.ray, 0.001f, T.te, t);
+                } else {
+                    hit = leaf_t<STATS>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st);
+                }
+                if (hit) {
+                    T.te = t;
+                    T.found = leaf;
+                }
+            }
+            if (!descended) {
+                if (T.sp == 0) T.phase = PH_SHADE;
+                else T.node = stack[(--T.sp) * RTW_BLOCK];
+            }
+        }
+    }
+    if (STATS) {
+        T.n_nodes = st.c[ST_NODES];
+        T.n_sph_rect = st.c[ST_T_SPHERE] | (st.c[ST_T_RECT] << 16);
+        T.n_box_tri = st.c[ST_T_BOX] | (st.c[ST_T_TRI] << 16);
+    }
+    return T;
+}
+
+template <bool STATS, bool LDS_SCENE>
+__global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
+    // LDS: [scene: nodes (2 float4 each) + leaf records (1 float4 each)] [stack: depth x BLOCK]
+    const DWorld& w = A.w;
+    if (LDS_SCENE) {
+        for (int i = threadIdx.x; i < 2 * A.node_count; i += RTW_BLOCK) smem[i] = w.node_a[i];
+        for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
+        __syncthreads();
+    }
+    Stats st;
+    if (STATS)
+        for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
+    const int lane = threadIdx.x & 63;
+    const int per_tile = A.tile_w * A.tile_h;
+
+    // Per-lane state machine.  Pixels come from a queue in tile order (wave-aggregated
+    // atomics); each lane iterates its pixel's samples in order (the per-pixel f32 sum is the
+    // reference's sequential .sum(), rendering.rs:172-179).
+    uint32_t pix = 0, slot = 0;
+    float fx = 0.0f, fy = 0.0f;
+    V3 sum = v3(0.0f, 0.0f, 0.0f);
+    uint32_t sample = 0;
+    V3 pdir = v3(0.0f, 0.0f, 0.0f), att = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
+    int32_t depth = 0;
+    Trav T;
+    T.phase = PH_PIXEL;
+    T.n_nodes = 0;
+    T.n_sph_rect = 0;
+    T.n_box_tri = 0;
+    T.node = 0;
+    T.sp = 0;
+    T.te = F32_INF;
+    T.found = -1;
+    bool fresh = false;  // T.ray is new: the traversal state must be initialised
+
+    // rendering.rs:174-176: jitter (x then y), then Camera::ray
+    auto start_sample = [&]() {
+        T.rng = rtw_sample_stream(A.seed_key, pix, sample);
+        const float jx = rtw_uniform_sample(&A.ux, &T.rng);
+        const float jy = rtw_uniform_sample(&A.uy, &T.rng);
+        T.ray = camera_ray(w.wc->cam, T.rng, fx + jx, fy + jy);
+        pdir = T.ray.d;
+        att = v3(1.0f, 1.0f, 1.0f);
+        acc = v3(0.0f, 0.0f, 0.0f);
+        depth = A.max_depth;
+        fresh = true;
+    };
+
+    for (;;) {
+        // 1. lanes without a pixel take the next ones (one atomic per wave per round)
+        bool out_of_work = false;
+        for (;;) {
+            const unsigned long long m = __ballot(T.phase == PH_PIXEL);
+            if (m == 0) break;
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned int base = 0;
+            if (lane == leader) base = atomicAdd(A.queue, (unsigned int)__popcll(m));
+            base = __shfl(base, leader);
+            if (T.phase == PH_PIXEL) {
+                const unsigned long long below = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
+                const uint32_t c = base + (uint32_t)__popcll(below);
+                if (c >= A.total) {
+                    out_of_work = true;
+                    T.phase = PH_TRACE;  // leaves the loops below
+                } else {
+                    const int32_t lt = (int32_t)(c / (uint32_t)per_tile);
+                    const int32_t it = (int32_t)(c % (uint32_t)per_tile);
+                    const int32_t tile = A.part_index + lt * A.part_count;
+                    const int32_t px = (tile % A.tiles_x) * A.tile_w + it % A.tile_w;
+                    const int32_t py = (tile / A.tiles_x) * A.tile_h + it / A.tile_w;
+                    if (px < A.width && py < A.height) {  // else: padding slot of an edge tile
+                        slot = c;
+                        pix = (uint32_t)(py * A.width + px);
+                        fx = (float)px * A.sx;  // size2i.rs:52-55
+                        fy = (float)py * A.sy;
+                        sum = v3(0.0f, 0.0f, 0.0f);
+                        sample = 0;
+                        start_sample();
+                        T.phase = PH_TRACE;
+                    }
+                }
+            }
+        }
+        if (out_of_work) break;
+
+        // 2. a new ray starts at the root (Scene::hit with t_range 0.001..inf, rendering.rs:25)
+        if (fresh) {
+            fresh = false;
+            const RayPre rp = ray_pre(T.ray);
+            T.inv = rp.inv;
+            T.fast = rp.fast ? 1 : 0;
+            T.node = w.root;
+            T.sp = 0;
+            T.te = F32_INF;
+            T.found = -1;
+            if (STATS) st.c[ST_RAYS]++;
+        }
+
+        // 3. traversal (hittable.rs:429-473)
+        T = traverse<STATS, LDS_SCENE>(A.wdev, T, A.trace_min, A.node_count, A.leaf_count);
+        if (STATS) {
+            st.c[ST_NODES] += T.n_nodes;
+            st.c[ST_T_SPHERE] += T.n_sph_rect & 0xFFFFu;
+            st.c[ST_T_RECT] += T.n_sph_rect >> 16;
+            st.c[ST_T_BOX] += T.n_box_tri & 0xFFFFu;
+            st.c[ST_T_TRI] += T.n_box_tri >> 16;
+        }
+
+        // 4. shade the lanes whose traversal finished (rendering.rs:19-71)
+        if (T.phase == PH_SHADE) {
+            if (STATS && T.found >= 0) {
+                st.c[ST_H_SPHERE + w.leaf_info[T.found].x]++;
+                st.c[ST_MAT]++;
+            }
+            Path P;
+            P.ray = T.ray;
+            P.att = att;
+            P.acc = acc;
+            P.depth = depth;
+            P.rng = T.rng;
+            const ShadeOut so = shade<STATS>(A.wdev, A.mode, P, T.found, T.te, pdir);
+            T.ray = so.p.ray;
+            att = so.p.att;
+            acc = so.p.acc;
+            depth = so.p.depth;
+            T.rng = so.p.rng;
+            if (STATS) st.c[ST_TEXEL] += so.texels;
+            T.phase = PH_TRACE;
+            if (so.done) {
+                sum = add(sum, so.color);
+                if (STATS) st.c[ST_SAMPLES]++;
+                ++sample;
+                if (sample >= A.spp) {
+                    // rendering.rs:179: sum / spp; merge_planes with one plane multiplies by 1.0
+                    const V3 pixel = divs(sum, (float)A.spp);
+                    float* o = (A.layout == RTW_LAYOUT_TILES) ? A.out + (int64_t)slot * 3 : A.out + (int64_t)pix * 3;
+                    o[0] = pixel.x;
+                    o[1] = pixel.y;
+                    o[2] = pixel.z;
+                    T.phase = PH_PIXEL;
+                } else {
+                    start_sample();
+                }
+            } else {
+                fresh = true;  // the scattered ray continues the path
             }
         }
     }
@@ -1070,6 +1234,7 @@ struct rtw_gpu_world {
     void* arena = nullptr;
     unsigned int* queue = nullptr;  // pixel work counter (one render at a time per world)
     DWorld w{};
+    const DWorld* wdev = nullptr;
     int32_t node_count = 0, leaf_count = 0, depth = 1;
     int cus = 0;
 };
@@ -1213,6 +1378,9 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     wcst.light = w->light;
     wcst.bg = w->background;
     const size_t o_wc = L.push(&wcst, sizeof(wcst));
+    DWorld dw_zero;
+    std::memset(&dw_zero, 0, sizeof(dw_zero));
+    const size_t o_dw = L.push(&dw_zero, sizeof(DWorld));  // filled once the pointers are known
 
     auto* g = new rtw_gpu_world;
     g->device = device;
@@ -1249,6 +1417,13 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     d.root = w->root;
     d.has_light = w->has_light;
     d.wc = (const WorldConst*)(base + o_wc);
+    e = hipMemcpy(base + o_dw, &g->w, sizeof(DWorld), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(g->arena);
+        delete g;
+        return rtw::fail(RTW_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    }
+    g->wdev = (const DWorld*)(base + o_dw);
     g->node_count = w->node_count;
     g->leaf_count = w->leaf_count;
     g->depth = std::max(1, depth);
@@ -1307,6 +1482,9 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.node_count = g->node_count;
     A.leaf_count = g->leaf_count;
     A.queue = g->queue;
+    A.wdev = g->wdev;
+    A.trace_min = 32;
+    if (const char* e = getenv("RTW_TRACE_MIN")) A.trace_min = atoi(e);
     A.seed_key = rtw_seed_key(p->seed);
     A.sx = 1.0f / (float)(p->width - 1);
     A.sy = 1.0f / (float)(p->height - 1);
