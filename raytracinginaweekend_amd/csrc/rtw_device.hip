@@ -452,7 +452,8 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
 // ---------------------------------------------------------------------------------------------
 // Exact f32 division by a ray-direction component d with y = RN(1/d) precomputed per ray
 // (Markstein): q = RN(a*y); r = fma(-d, q, a) (exact); q' = RN(q + r*y) == RN(a/d), provided
-// no underflow/overflow: the caller guarantees 2^-60 <= |d| <= 2, 2^-40 <= |a| <= 2^40
+// no underflow/overflow: the caller guarantees 2^-60 <= |d| <= 2, 2^-40 <= |a| <= 2^40 (the
+// upper bound holds by construction: world coordinates are bounded by 2^30 at upload)
 // (tests/native/markstein_check.c checks every divisor significand under these guards).
 #define RTW_MK_DMIN 0x1p-60f
 #define RTW_MK_AMIN 0x1p-40f
@@ -496,11 +497,9 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, const Ray& r, co
     const float lo = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fabsf(a0), __builtin_fabsf(b0)),
                                                      __builtin_fminf(__builtin_fabsf(a1), __builtin_fabsf(b1))),
                                      __builtin_fminf(__builtin_fabsf(a2), __builtin_fabsf(b2)));
-    const float hi = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(a0), __builtin_fabsf(b0)),
-                                                     __builtin_fmaxf(__builtin_fabsf(a1), __builtin_fabsf(b1))),
-                                     __builtin_fmaxf(__builtin_fabsf(a2), __builtin_fabsf(b2)));
+    // |a| <= 2^32 always: rtw_world_upload bounds every coordinate by 2^30 (check_world)
     float qa0, qb0, qa1, qb1, qa2, qb2;
-    if (__builtin_expect(rp.fast && lo >= RTW_MK_AMIN && hi <= RTW_MK_AMAX, 1)) {
+    if (__builtin_expect(rp.fast && lo >= RTW_MK_AMIN, 1)) {
         qa0 = mk_div(a0, r.d.x, rp.inv.x);
         qb0 = mk_div(b0, r.d.x, rp.inv.x);
         qa1 = mk_div(a1, r.d.y, rp.inv.y);
@@ -516,53 +515,6 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, const Ray& r, co
         qb2 = b2 / r.d.z;
     }
     return axis_pass(qa0, qb0, ts, te) && axis_pass(qa1, qb1, ts, te) && axis_pass(qa2, qb2, ts, te);
-}
-
-// Closest hit.  Returns the leaf index or -1; `te` is shrunk to the hit's t.  `nodes` holds
-// two float4 per node {min.xyz, max.x}, {max.y, max.z, left<<2|axis, right}; `fast` one float4
-// per leaf (plain spheres inline, w = NaN otherwise) -- both in LDS when they fit.
-template <bool STATS>
-__device__ __forceinline__ int trace(const DWorld& w, const float4* nodes, const float4* fast, const Ray& r, float ts,
-                                     float& te, rtw_xoro& rng, int32_t* stack, Stats& st) {
-    const RayPre rp = ray_pre(r);
-    int found = -1;
-    int32_t node = w.root;
-    int sp = 0;
-    for (;;) {
-        if (node < 0) {
-            const int leaf = -1 - node;
-            const float4 sph = fast[leaf];
-            float t;
-            bool hit;
-            if (sph.w == sph.w) {  // a plain sphere leaf
-                if (STATS) st.c[ST_T_SPHERE]++;
-                hit = sphere_t(sph, r, ts, te, t);
-            } else {
-                hit = leaf_t<STATS>(w, leaf, r, ts, te, rng, t, st);
-            }
-            if (hit) {
-                te = t;
-                found = leaf;
-            }
-        } else {
-            if (STATS) st.c[ST_NODES]++;
-            const float4 na = nodes[2 * node];
-            const float4 nb = nodes[2 * node + 1];
-            if (node_pass(na, nb, r, rp, ts, te)) {
-                const int32_t lbits = __float_as_int(nb.z);
-                const int32_t left = lbits >> 2;
-                const int axis = lbits & 3;
-                const int32_t right = __float_as_int(nb.w);
-                const bool fwd = comp(r.d, axis) > 0.0f;
-                stack[(sp++) * RTW_BLOCK] = fwd ? right : left;
-                node = fwd ? left : right;
-                continue;
-            }
-        }
-        if (sp == 0) break;
-        node = stack[(--sp) * RTW_BLOCK];
-    }
-    return found;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -865,11 +817,22 @@ struct Trav {
 // The hot loop: every lane in PH_TRACE advances one node or leaf per iteration until fewer than
 // `trace_min` lanes are still tracing while some lane waits for shading (dynamic ray fetch).
 // Out of line so that it gets a register allocation of its own.
+// A plain-sphere leaf test with the current range; updates te/found on a hit.
+__device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, float& te, int32_t& found) {
+    float t;
+    if (sphere_t(sph, r, 0.001f, te, t)) {
+        te = t;
+        found = leaf;
+    }
+}
+
 template <bool STATS, bool LDS_SCENE>
 __device__ __noinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
                                       int32_t n_leaves) {
     const DWorld& w = *wp;
-    const float4* nodes = LDS_SCENE ? smem : w.node_a;
+    // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
+    const float4* nodes_a = LDS_SCENE ? smem : w.node_a;
+    const float4* nodes_b = LDS_SCENE ? smem + n_nodes : w.node_b;
     const float4* fast = LDS_SCENE ? smem + 2 * n_nodes : w.leaf_fast;
     int32_t* stack = reinterpret_cast<int32_t*>(smem + (LDS_SCENE ? 2 * n_nodes + n_leaves : 0)) + threadIdx.x;
     Stats st;
@@ -881,38 +844,64 @@ __device__ __noinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int
         if (tr == 0) break;
         if (__popcll(tr) < (unsigned)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
         if (T.phase == PH_TRACE) {
-            bool descended = false;
+            bool next_set = false;  // T.node already holds the next item to visit
             if (T.node >= 0) {
                 if (STATS) st.c[ST_NODES]++;
-                const float4 na = nodes[2 * T.node];
-                const float4 nb = nodes[2 * T.node + 1];
+                const float4 na = nodes_a[T.node];
+                const float4 nb = nodes_b[T.node];
                 if (node_pass(na, nb, T.ray, rp, 0.001f, T.te)) {
                     const int32_t lbits = __float_as_int(nb.z);
                     const int32_t left = lbits >> 2;
                     const int axis = lbits & 3;
                     const int32_t right = __float_as_int(nb.w);
                     const bool fwd = comp(T.ray.d, axis) > 0.0f;
-                    stack[(T.sp++) * RTW_BLOCK] = fwd ? right : left;
-                    T.node = fwd ? left : right;
-                    descended = true;
+                    const int32_t near = fwd ? left : right;
+                    const int32_t far = fwd ? right : left;
+                    // hit_index_list order: near subtree, then far.  A plain-sphere leaf child is
+                    // tested right here (same order, same t_range), saving a divergent iteration.
+                    float4 sn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    bool near_fast = false;
+                    if (near < 0) {
+                        sn = fast[-1 - near];
+                        near_fast = sn.w == sn.w;
+                    }
+                    if (near_fast) {
+                        if (STATS) st.c[ST_T_SPHERE]++;
+                        sphere_leaf(sn, -1 - near, T.ray, T.te, T.found);
+                        bool far_fast = false;
+                        float4 sf = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        if (far < 0) {
+                            sf = fast[-1 - far];
+                            far_fast = sf.w == sf.w;
+                        }
+                        if (far_fast) {
+                            if (STATS) st.c[ST_T_SPHERE]++;
+                            sphere_leaf(sf, -1 - far, T.ray, T.te, T.found);
+                        } else {
+                            T.node = far;
+                            next_set = true;
+                        }
+                    } else {
+                        stack[(T.sp++) * RTW_BLOCK] = far;
+                        T.node = near;
+                        next_set = true;
+                    }
                 }
             } else {
                 const int leaf = -1 - T.node;
                 const float4 sph = fast[leaf];
-                float t;
-                bool hit;
-                if (sph.w == sph.w) {  // a plain sphere leaf
+                if (sph.w == sph.w) {  // a plain sphere leaf (only reached as the root or via the stack)
                     if (STATS) st.c[ST_T_SPHERE]++;
-                    hit = sphere_t(sph, T.ray, 0.001f, T.te, t);
+                    sphere_leaf(sph, leaf, T.ray, T.te, T.found);
                 } else {
-                    hit = leaf_t<STATS>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st);
-                }
-                if (hit) {
-                    T.te = t;
-                    T.found = leaf;
+                    float t;
+                    if (leaf_t<STATS>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) {
+                        T.te = t;
+                        T.found = leaf;
+                    }
                 }
             }
-            if (!descended) {
+            if (!next_set) {
                 if (T.sp == 0) T.phase = PH_SHADE;
                 else T.node = stack[(--T.sp) * RTW_BLOCK];
             }
@@ -931,7 +920,10 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
     // LDS: [scene: nodes (2 float4 each) + leaf records (1 float4 each)] [stack: depth x BLOCK]
     const DWorld& w = A.w;
     if (LDS_SCENE) {
-        for (int i = threadIdx.x; i < 2 * A.node_count; i += RTW_BLOCK) smem[i] = w.node_a[i];
+        for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) {
+            smem[i] = w.node_a[i];
+            smem[A.node_count + i] = w.node_b[i];
+        }
         for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
         __syncthreads();
     }
@@ -1261,15 +1253,15 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
 
     Layout L;
     // nodes
-    // nodes: two float4 per node, interleaved (one 32-byte record)
-    std::vector<float4> na((size_t)std::max(1, 2 * w->node_count));
+    // nodes: two SoA float4 halves {min.xyz, max.x}, {max.y, max.z, left<<2|axis, right}
+    std::vector<float4> na((size_t)std::max(1, w->node_count)), nb((size_t)std::max(1, w->node_count));
     for (int i = 0; i < w->node_count; ++i) {
         const rtw_bvh_node& n = w->nodes[i];
-        na[2 * (size_t)i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
-        na[2 * (size_t)i + 1] =
-            make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
+        na[(size_t)i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
+        nb[(size_t)i] = make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
     }
     const size_t o_na = L.push(na.data(), na.size() * sizeof(float4));
+    const size_t o_nb = L.push(nb.data(), nb.size() * sizeof(float4));
     // leaf records for the traversal: plain spheres inline, everything else tagged NaN
     std::vector<float4> lf((size_t)w->leaf_count);
     for (int i = 0; i < w->leaf_count; ++i) {
@@ -1398,7 +1390,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     uint8_t* base = (uint8_t*)g->arena;
     DWorld& d = g->w;
     d.node_a = (const float4*)(base + o_na);
-    d.node_b = nullptr;
+    d.node_b = (const float4*)(base + o_nb);
     d.leaf_fast = (const float4*)(base + o_lf);
     d.leaf_info = (const int4*)(base + o_li);
     d.leaf_xf = (const float4*)(base + o_lx);
