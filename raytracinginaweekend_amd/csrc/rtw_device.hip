@@ -463,16 +463,16 @@ __device__ __forceinline__ float mk_div(float a, float d, float y) {
     return __builtin_fmaf(__builtin_fmaf(-d, q, a), y, q);
 }
 
-// One axis of Aabb::hit_cond: minmax (math.rs:35-41), then !(min(t1, te) <= max(t0, ts)).
-// tmin/tmax are never NaN (te, ts are not; Rust's min/max drop a NaN operand), so the test is
-// tmax > tmin, and min/max of a value against ts = 0.001 or te > 0 cannot meet the +-0 case.
+// One axis of Aabb::hit_cond (aabb.rs:65-78): (t0, t1) = minmax(qa, qb) (math.rs:35-41: `a < b`
+// else swapped, so a NaN lands in t1 position of qa), tmin = max(t0, ts), tmax = min(t1, te) with
+// Rust's NaN-dropping min/max, pass = !(tmax <= tmin).  te and ts are never NaN, so
+//   pass <=> te > ts  &&  !(t1 <= ts)  &&  !(te <= t0)  &&  !(t1 <= t0)
+// and !(t1 <= t0) <=> qa != qb (unordered-true).  The te > ts term is per node (node_pass).
 __device__ __forceinline__ bool axis_pass(float qa, float qb, float ts, float te) {
     const bool lt = qa < qb;
     const float t0 = lt ? qa : qb;
     const float t1 = lt ? qb : qa;
-    const float tmax = (t1 < te) ? t1 : te;
-    const float tmin = (t0 > ts) ? t0 : ts;
-    return tmax > tmin;
+    return (int)!(t1 <= ts) & (int)!(te <= t0) & (int)(qa != qb);  // non-short-circuit
 }
 
 struct RayPre {  // per-ray constants of the slab test
@@ -514,7 +514,9 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, const Ray& r, co
         qa2 = a2 / r.d.z;
         qb2 = b2 / r.d.z;
     }
-    return axis_pass(qa0, qb0, ts, te) && axis_pass(qa1, qb1, ts, te) && axis_pass(qa2, qb2, ts, te);
+    // all three axes evaluated (no short-circuit): one predicate instead of three nested branches
+    return (int)(te > ts) & (int)axis_pass(qa0, qb0, ts, te) & (int)axis_pass(qa1, qb1, ts, te) &
+           (int)axis_pass(qa2, qb2, ts, te);
 }
 
 // ---------------------------------------------------------------------------------------------
