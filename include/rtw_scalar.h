@@ -471,6 +471,26 @@ RTW_HD float rtw_sinf(float x) {
     return (float)v;
 }
 
+
+/* ------------------------------------------------------------------------------------------ */
+/* Proximity cull (ours, not in the reference): an extra per-node test ANDed with the          */
+/* reference's Aabb::hit_cond.  It never rejects a node below which a cullable leaf's test     */
+/* would accept a root in [ts, te), so the closest hit, its tie-breaking and every RNG draw     */
+/* are those of the reference traversal (argument and error bounds: DESIGN.md "Proximity       */
+/* cull"; node constants k, m: rtw_cull.h).                                                     */
+/*   per (ray, node): D = sum_i max(|min_i - o_i|, |max_i - o_i|) >= |o - x| for every x in    */
+/*   the box; delta = k D^2 + 64u D + m bounds how far outside the box a computed hit point of  */
+/*   a leaf below can lie (plus the quotient roundings); the node passes when the ray segment   */
+/*   [ts, te] meets the box grown by delta, reusing hit_cond's slab quotients.                  */
+/* ------------------------------------------------------------------------------------------ */
+#define RTW_CULL_U 0x1p-24f
+RTW_HD float rtw_cull_delta(float k, float m, float d) { return (k * d) * d + ((64.0f * RTW_CULL_U) * d + m); }
+/* one axis: [t0 - w, t1 + w] narrows [lo, hi]; NaN operands are dropped (conservative) */
+RTW_HD void rtw_cull_axis(float t0, float t1, float w, float* lo, float* hi) {
+    *lo = __builtin_fmaxf(*lo, t0 - w);
+    *hi = __builtin_fminf(*hi, t1 + w);
+}
+
 #ifdef __cplusplus
 }
 #endif

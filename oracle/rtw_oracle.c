@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include "../include/rtw_scalar.h"
+#include "../include/rtw_cull.h"
 
 #define F32_PI 3.14159274101257324219f  /* std::f32::consts::PI */
 #define F32_TAU 6.28318548202514648438f /* std::f32::consts::TAU */
@@ -99,6 +100,7 @@ typedef struct Ctx {
     const rtw_world* w;
     rtw_xoro* rng;
     Stats* st; /* may be NULL */
+    const float* km; /* proximity-cull node constants (rtw_cull.h), NULL = reference traversal */
 } Ctx;
 
 /* ------------------------------------------------------------------------------------------ */
@@ -371,6 +373,25 @@ static int aabb_hit_cond(const rtw_bvh_node* nd, const Ray* r, float ts, float t
     return 1;
 }
 
+/* The product's extra proximity test (rtw_scalar.h rtw_cull_*; NOT part of the reference):
+ * RTW_ORACLE_CULL mode applies it after hit_cond to check, on the CPU, that it changes no
+ * result and to count the culled traversal's work. */
+static int cull_pass(const float* km, int32_t n, const rtw_bvh_node* nd, const Ray* r, float ts, float te) {
+    float d = 0.0f, t0[3], t1[3];
+    for (int i = 0; i < 3; ++i) {
+        const float a = nd->min[i] - r->origin.e[i];
+        const float b = nd->max[i] - r->origin.e[i];
+        d += fmaxf(fabsf(a), fabsf(b));
+        const float qa = a / r->dir.e[i], qb = b / r->dir.e[i];
+        t0[i] = (qa < qb) ? qa : qb;
+        t1[i] = (qa < qb) ? qb : qa;
+    }
+    const float delta = rtw_cull_delta(km[2 * (size_t)n], km[2 * (size_t)n + 1], d);
+    float lo = ts, hi = te;
+    for (int i = 0; i < 3; ++i) rtw_cull_axis(t0[i], t1[i], delta * fabsf(1.0f / r->dir.e[i]), &lo, &hi);
+    return lo <= hi;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* texture.rs + perlin.rs                                                                      */
 /* ------------------------------------------------------------------------------------------ */
@@ -622,6 +643,7 @@ static int bvh_closest_leaf_recursive(const Ctx* c, int32_t node, const Ray* r, 
     const rtw_bvh_node* nd = &c->w->nodes[node];
     if (c->st) c->st->node_visits++;
     if (!aabb_hit_cond(nd, r, ts, *te)) return 0;
+    if (c->km && !cull_pass(c->km, node, nd, r, ts, *te)) return 0;
     if (r->dir.e[nd->axis] > 0.0f) return bvh_list_leaf(c, nd->left, nd->right, r, ts, te, h, leaf);
     return bvh_list_leaf(c, nd->right, nd->left, r, ts, te, h, leaf);
 }
@@ -730,6 +752,7 @@ typedef struct Job {
     const rtw_world* w;
     const rtw_render_params* p;
     int mode; /* rng mode */
+    const float* km; /* proximity cull constants or NULL */
     float* out;
     /* ctr */
     int row_begin, row_step;
@@ -763,6 +786,7 @@ static void* ctr_worker(void* arg) {
     c.w = j->w;
     c.rng = &rng;
     c.st = j->want_stats ? &j->st : NULL;
+    c.km = j->km;
     for (int y = j->row_begin; y < H; y += j->row_step) {
         for (int x = 0; x < W; ++x) {
             if (!tile_owned(p, x, y)) continue;
@@ -800,6 +824,7 @@ static void* ref_worker(void* arg) {
     c.w = j->w;
     c.rng = &rng;
     c.st = j->want_stats ? &j->st : NULL;
+    c.km = j->km;
     for (int y = 0; y < H; ++y) {
         for (int x = 0; x < W; ++x) {
             const float fx = (float)x * sx, fy = (float)y * sy;
@@ -853,6 +878,12 @@ RTW_API int rtw_oracle_render(const rtw_world* w, const rtw_render_params* p, in
     if (!out_rgb) return RTW_ERR_INVALID_ARGUMENT;
     if (threads < 1) threads = 1;
     if (stats) memset(stats, 0, sizeof(*stats));
+    float* km = NULL;
+    if (rng_mode & RTW_ORACLE_CULL) {
+        km = (float*)malloc(sizeof(float) * 2u * (size_t)(w->node_count > 0 ? w->node_count : 1));
+        rtw_cull_prepare(w, km, 0);
+    }
+    rng_mode &= ~RTW_ORACLE_CULL;
     const size_t n = (size_t)p->width * (size_t)p->height * 3u;
     if (rng_mode == RTW_ORACLE_RNG_CTR) {
         Job* jobs = (Job*)calloc((size_t)threads, sizeof(Job));
@@ -864,6 +895,7 @@ RTW_API int rtw_oracle_render(const rtw_world* w, const rtw_render_params* p, in
             jobs[t].row_begin = t;
             jobs[t].row_step = threads;
             jobs[t].want_stats = stats != NULL;
+            jobs[t].km = km;
             pthread_create(&th[t], NULL, ctr_worker, &jobs[t]);
         }
         for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
@@ -871,6 +903,7 @@ RTW_API int rtw_oracle_render(const rtw_world* w, const rtw_render_params* p, in
             for (int t = 0; t < threads; ++t) add_stats(stats, &jobs[t].st);
         free(th);
         free(jobs);
+        free(km);
         return RTW_OK;
     }
     /* ref mode: split_work_tasks (rendering.rs:222-237) */
@@ -893,6 +926,7 @@ RTW_API int rtw_oracle_render(const rtw_world* w, const rtw_render_params* p, in
         jobs[t].thread_id = (uint32_t)t;
         jobs[t].spp_t = whole + ((uint32_t)t < rem ? 1u : 0u);
         jobs[t].want_stats = stats != NULL;
+        jobs[t].km = km;
         pthread_create(&th[t], NULL, ref_worker, &jobs[t]);
     }
     for (int t = 0; t < nt; ++t) pthread_join(th[t], NULL);
@@ -908,6 +942,7 @@ RTW_API int rtw_oracle_render(const rtw_world* w, const rtw_render_params* p, in
     free(planes);
     free(th);
     free(jobs);
+    free(km);
     return RTW_OK;
 }
 
@@ -918,7 +953,7 @@ RTW_API int rtw_oracle_scene_hit(const rtw_world* w, const float origin[3], cons
                                  float t_start, float t_end, uint64_t rng_state[2], rtw_oracle_hit* out) {
     if (!w || !out || w->leaf_count < 1) return RTW_ERR_INVALID_ARGUMENT;
     rtw_xoro rng = {rng_state[0], rng_state[1]};
-    Ctx c = {w, &rng, NULL};
+    Ctx c = {w, &rng, NULL, NULL};
     Ray r;
     r.origin = vload(origin);
     r.dir = vload(dir);
@@ -962,7 +997,7 @@ RTW_API int rtw_oracle_ray_color(const rtw_world* w, const float origin[3], cons
                                  int32_t max_depth, int32_t mode, uint64_t rng_state[2], float color[3]) {
     if (!w || w->leaf_count < 1) return RTW_ERR_INVALID_ARGUMENT;
     rtw_xoro rng = {rng_state[0], rng_state[1]};
-    Ctx c = {w, &rng, NULL};
+    Ctx c = {w, &rng, NULL, NULL};
     Ray r;
     r.origin = vload(origin);
     r.dir = vload(dir);

@@ -21,6 +21,10 @@ extern "C" {
 
 #define RTW_ORACLE_RNG_CTR 0 /* per-(pixel, sample) streams: the device kernel's semantics */
 #define RTW_ORACLE_RNG_REF 1 /* per-thread streams + sample split + merge_planes (rendering.rs) */
+/* OR-ed into rng_mode: also apply the product's proximity cull (rtw_cull.h) after hit_cond.
+ * Not the reference's traversal: used to check that the cull changes no result and to count
+ * the culled traversal's work (the device kernel's statistics). */
+#define RTW_ORACLE_CULL 0x100
 
 /* rendering::render restated.  ctr mode: `threads` only parallelises over rows (result is
  * independent of it); honours the tile partition in params (owned tiles only, image layout).

@@ -239,6 +239,8 @@ _SIGS = {
     "rtw_partition_floats": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int64)]),
     "rtw_untile_device": (C.c_int, [C.POINTER(RenderParams), _P, C.c_int64, _P, _P]),
     "rtw_render_collect_stats": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(RenderStats)]),
+    "rtw_render_debug_counters": (
+        C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(RenderStats), C.POINTER(C.c_uint64), C.c_int]),
     "rtw_encode_rgb8_device": (C.c_int, [_P, C.c_int64, _P, _P]),
     "rtw_device_eval_scalar": (
         C.c_int,

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/rtw_scalar.h"
+#include "../../include/rtw_cull.h"
 #include "rtw_common.h"
 
 #define RTW_BLOCK 512   // 8 waves; 2 blocks per CU at <= 128 VGPRs -> 4 waves per SIMD
@@ -39,13 +40,14 @@ namespace {
 struct DWorld {
     const float4* node_a;  // {min.x, min.y, min.z, max.x}
     const float4* node_b;  // {max.y, max.z, bits(left << 2 | axis), bits(right)}
+    const float2* node_km; // proximity-cull constants {k, m} (rtw_cull.h)
     const int4* leaf_info; // {geom_kind, geom_index, material, flags}
-    const float4* leaf_fast; // plain sphere leaves: {center.xyz, radius}; other leaves: w = NaN
+    const float4* leaf_fast; // plain sphere: {center.xyz, radius}; else w = NaN, x = bits(1) for a plain triangle (y = index)
     const float4* leaf_xf; // 3 per leaf: {neg_inv_density, off.xyz}, {ys, yc, vel.x, vel.y}, {vel.z,0,0,0}
     const float4* spheres; // {center.xyz, radius}
     const float4* rects;   // 2 per rect: {dist, r0.0, r0.1, r1.0}, {r1.1, bits(plane), 0, 0}
     const float4* boxes;   // 2 per box: {min.xyz, max.x}, {max.y, max.z, 0, 0}
-    const float4* tri_pos; // 3 per tri: {p0.xyz, p1.x}, {p1.yz, p2.xy}, {p2.z, 0, 0, 0}
+    const float4* tri_fast; // 4 per tri: ray-independent part of the test (TriFast)
     const float4* tri_attr; // 4 per tri: normals and uvs packed
     const int4* materials; // {kind, texture, bits(fuzz), bits(ior)}
     const int4* textures;  // 3 per texture
@@ -78,7 +80,13 @@ struct KArgs {
     int32_t part_index, part_count;
     uint32_t total;          // pixel slots in this partition (owned tiles * tile_w * tile_h)
     int32_t node_count, leaf_count;
-    unsigned int* queue;     // pixel work counter (zeroed before each launch)
+    unsigned long long* queue; // work-item counter (zeroed before each launch)
+    // one launch renders samples [s_begin, s_end) of every slot as work items of `chunk`
+    // consecutive samples (item = chunk index * total + slot); each finished sample's colour goes
+    // to colors[(sample - s_begin) * total + slot] and accumulate_kernel sums them in order
+    uint32_t s_begin, s_end, chunk;
+    uint64_t items;
+    float* colors;
     int32_t trace_min;       // dynamic ray fetch threshold (lanes still tracing)
     const DWorld* wdev;      // a copy of `w` in device memory (for the out-of-line shader)
     uint64_t seed_key;
@@ -94,19 +102,19 @@ struct KArgs {
 struct V3 {
     float x, y, z;
 };
-__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__host__ __device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__host__ __device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__host__ __device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ V3 mul(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__host__ __device__ __forceinline__ V3 mul(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ V3 divs(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ V3 conv(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+__host__ __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ __forceinline__ V3 cross(V3 a, V3 b) {
     return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-__device__ __forceinline__ float len(V3 a) { return __builtin_sqrtf(dot(a, a)); }
-__device__ __forceinline__ V3 unit(V3 a) { return mul(a, 1.0f / len(a)); }  // vec3.rs:205-210
+__host__ __device__ __forceinline__ float len(V3 a) { return __builtin_sqrtf(dot(a, a)); }
+__host__ __device__ __forceinline__ V3 unit(V3 a) { return mul(a, 1.0f / len(a)); }  // vec3.rs:205-210
 __device__ __forceinline__ float comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 __device__ __forceinline__ void setc(V3& a, int i, float v) {
     if (i == 0) a.x = v;
@@ -147,6 +155,11 @@ enum {
     ST_SAMPLES, ST_RAYS, ST_NODES, ST_T_SPHERE, ST_T_RECT, ST_T_BOX, ST_T_TRI,
     ST_H_SPHERE, ST_H_RECT, ST_H_BOX, ST_H_TRI, ST_MAT, ST_TEXEL, ST_COUNT
 };
+// wave-level execution counters of the counting variant (rtw_render_debug_counters), stored
+// after the ST_COUNT statistics: traversal calls / loop iterations / iterations that ran the node
+// resp. leaf path / lanes stepping a node resp. a leaf / shade calls / lanes shading
+enum { DB_TRAV_CALLS, DB_ITERS, DB_NODE_ITERS, DB_LEAF_ITERS, DB_NODE_LANES, DB_LEAF_LANES, DB_ALIVE_LANES,
+       DB_WAIT_LANES, DB_SHADE_CALLS, DB_SHADE_LANES, DB_COUNT };
 struct Stats {
     uint32_t c[ST_COUNT];
 };
@@ -241,31 +254,50 @@ __device__ __forceinline__ bool box_t(const DWorld& w, int i, const Ray& r, floa
     return false;
 }
 
-struct TriP {
-    V3 p0, p1, p2;
+// triangle_geometry.rs:13-45.  Everything that does not depend on the ray -- the edges, the
+// unit normal, the two barycentric axes and their denominators -- is computed once at upload with
+// the same f32 operations in the same order (host and device share these helpers; both are
+// IEEE f32 without contraction), so the values are bit-identical to the reference's per-test ones.
+struct TriFast {
+    V3 p0, n, vt1, vt2;
+    float den1, den2;
 };
-__device__ __forceinline__ TriP load_tri(const DWorld& w, int i) {
-    const float4 a = w.tri_pos[3 * i], b = w.tri_pos[3 * i + 1], c = w.tri_pos[3 * i + 2];
-    return TriP{v3(a.x, a.y, a.z), v3(a.w, b.x, b.y), v3(b.z, b.w, c.x)};
+__host__ __device__ __forceinline__ TriFast tri_prepare(V3 p0, V3 p1, V3 p2) {
+    TriFast f;
+    const V3 dir1 = sub(p1, p0);
+    const V3 dir2 = sub(p2, p0);
+    f.p0 = p0;
+    f.n = unit(cross(dir1, dir2));
+    f.vt1 = cross(f.n, dir2);
+    f.den1 = dot(dir1, f.vt1);
+    f.vt2 = cross(f.n, dir1);
+    f.den2 = dot(dir2, f.vt2);
+    return f;
 }
-// triangle_geometry.rs:13-45; returns barycentrics for the record pass
-__device__ __forceinline__ bool tri_test(const TriP& T, const Ray& r, float ts, float te, float& t, V3& pos,
-                                         float& w0, float& w1, float& w2) {
-    const V3 dir1 = sub(T.p1, T.p0);
-    const V3 dir2 = sub(T.p2, T.p0);
-    const V3 normal = unit(cross(dir1, dir2));
-    const float denom = dot(r.d, normal);
+// 4 float4 per triangle: {p0.xyz, n.x} {n.yz, vt1.xy} {vt1.z, den1, vt2.xy} {vt2.z, den2, 0, 0}
+__device__ __forceinline__ TriFast load_tri(const DWorld& w, int i) {
+    const float4 a = w.tri_fast[4 * i], b = w.tri_fast[4 * i + 1], c = w.tri_fast[4 * i + 2],
+                 d = w.tri_fast[4 * i + 3];
+    TriFast f;
+    f.p0 = v3(a.x, a.y, a.z);
+    f.n = v3(a.w, b.x, b.y);
+    f.vt1 = v3(b.z, b.w, c.x);
+    f.den1 = c.y;
+    f.vt2 = v3(c.z, c.w, d.x);
+    f.den2 = d.y;
+    return f;
+}
+// the per-ray part; barycentrics are recomputed from (ray, t) by leaf_record
+__device__ __forceinline__ bool tri_test(const TriFast& T, const Ray& r, float ts, float te, float& t) {
+    const float denom = dot(r.d, T.n);
     if (!(__builtin_fabsf(denom) > 0.0001f)) return false;
-    t = dot(sub(T.p0, r.o), normal) / denom;
+    t = dot(sub(T.p0, r.o), T.n) / denom;
     if (!contains(ts, te, t)) return false;
-    pos = at(r, t);
-    const V3 q = sub(pos, T.p0);
-    V3 vt = cross(normal, dir2);
-    w1 = dot(q, vt) / dot(dir1, vt);
+    const V3 q = sub(at(r, t), T.p0);
+    const float w1 = dot(q, T.vt1) / T.den1;
     if (!(w1 > 0.0f && w1 < 1.0f)) return false;
-    vt = cross(normal, dir1);
-    w2 = dot(q, vt) / dot(dir2, vt);
-    w0 = 1.0f - w1 - w2;
+    const float w2 = dot(q, T.vt2) / T.den2;
+    const float w0 = 1.0f - w1 - w2;
     return w2 > 0.0f && w0 > 0.0f;
 }
 
@@ -279,9 +311,7 @@ __device__ __forceinline__ bool geom_t(const DWorld& w, int kind, int idx, const
         return rect_t(load_rect(w, idx), r, ts, te, t, pos);
     }
     if (kind == RTW_GEOM_BOX) return box_t(w, idx, r, ts, te, t);
-    V3 pos;
-    float w0, w1, w2;
-    return tri_test(load_tri(w, idx), r, ts, te, t, pos, w0, w1, w2);
+    return tri_test(load_tri(w, idx), r, ts, te, t);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -409,21 +439,12 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         setc(sn, plane, rtw_signum(comp(pos, plane) - center));
         from_ray(h, rr, pos, sn, 0.0f, 0.0f);
     } else {  // triangle_geometry.rs:22-39
-        const TriP T = load_tri(w, idx);
-        float w0, w1, w2;
+        const TriFast T = load_tri(w, idx);
         const V3 pos = at(rr, t);
-        {
-            // recompute barycentrics from the final t exactly as the test did
-            const V3 dir1 = sub(T.p1, T.p0);
-            const V3 dir2 = sub(T.p2, T.p0);
-            const V3 normal = unit(cross(dir1, dir2));
-            const V3 q = sub(pos, T.p0);
-            V3 vt = cross(normal, dir2);
-            w1 = dot(q, vt) / dot(dir1, vt);
-            vt = cross(normal, dir1);
-            w2 = dot(q, vt) / dot(dir2, vt);
-            w0 = 1.0f - w1 - w2;
-        }
+        const V3 q = sub(pos, T.p0);
+        const float w1 = dot(q, T.vt1) / T.den1;
+        const float w2 = dot(q, T.vt2) / T.den2;
+        const float w0 = 1.0f - w1 - w2;
         const float4 a0 = w.tri_attr[4 * idx], a1 = w.tri_attr[4 * idx + 1], a2 = w.tri_attr[4 * idx + 2],
                      a3 = w.tri_attr[4 * idx + 3];
         const V3 n0 = v3(a0.x, a0.y, a0.z), n1 = v3(a0.w, a1.x, a1.y), n2 = v3(a1.z, a1.w, a2.x);
@@ -490,13 +511,19 @@ __device__ __forceinline__ RayPre ray_pre(const Ray& r) {
     return p;
 }
 
-__device__ __forceinline__ bool node_pass(float4 na, float4 nb, const Ray& r, const RayPre& rp, float ts, float te) {
+// Aabb::hit_cond (exact quotients) AND the proximity cull (rtw_scalar.h rtw_cull_*), which
+// reuses the same quotients: pass iff the segment [ts, te] meets the box grown by delta.
+__device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const Ray& r, const RayPre& rp, float ts,
+                                          float te) {
     const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
     const float lo = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fabsf(a0), __builtin_fabsf(b0)),
                                                      __builtin_fminf(__builtin_fabsf(a1), __builtin_fabsf(b1))),
                                      __builtin_fminf(__builtin_fabsf(a2), __builtin_fabsf(b2)));
+    const float dsum = (__builtin_fmaxf(__builtin_fabsf(a0), __builtin_fabsf(b0)) +
+                        __builtin_fmaxf(__builtin_fabsf(a1), __builtin_fabsf(b1))) +
+                       __builtin_fmaxf(__builtin_fabsf(a2), __builtin_fabsf(b2));
     // |a| <= 2^32 always: rtw_world_upload bounds every coordinate by 2^30 (check_world)
     float qa0, qb0, qa1, qb1, qa2, qb2;
     if (__builtin_expect(rp.fast && lo >= RTW_MK_AMIN, 1)) {
@@ -515,8 +542,14 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, const Ray& r, co
         qb2 = b2 / r.d.z;
     }
     // all three axes evaluated (no short-circuit): one predicate instead of three nested branches
-    return (int)(te > ts) & (int)axis_pass(qa0, qb0, ts, te) & (int)axis_pass(qa1, qb1, ts, te) &
-           (int)axis_pass(qa2, qb2, ts, te);
+    const int hit_cond = (int)(te > ts) & (int)axis_pass(qa0, qb0, ts, te) & (int)axis_pass(qa1, qb1, ts, te) &
+                         (int)axis_pass(qa2, qb2, ts, te);
+    const float delta = rtw_cull_delta(km.x, km.y, dsum);
+    float clo = ts, chi = te;
+    rtw_cull_axis(qa0 < qb0 ? qa0 : qb0, qa0 < qb0 ? qb0 : qa0, delta * __builtin_fabsf(rp.inv.x), &clo, &chi);
+    rtw_cull_axis(qa1 < qb1 ? qa1 : qb1, qa1 < qb1 ? qb1 : qa1, delta * __builtin_fabsf(rp.inv.y), &clo, &chi);
+    rtw_cull_axis(qa2 < qb2 ? qa2 : qb2, qa2 < qb2 ? qb2 : qa2, delta * __builtin_fabsf(rp.inv.z), &clo, &chi);
+    return hit_cond & (int)(clo <= chi);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -830,28 +863,44 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 
 template <bool STATS, bool LDS_SCENE>
 __device__ __noinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
-                                      int32_t n_leaves) {
+                                      int32_t n_leaves, unsigned long long* dbg) {
     const DWorld& w = *wp;
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
     const float4* nodes_a = LDS_SCENE ? smem : w.node_a;
     const float4* nodes_b = LDS_SCENE ? smem + n_nodes : w.node_b;
     const float4* fast = LDS_SCENE ? smem + 2 * n_nodes : w.leaf_fast;
-    int32_t* stack = reinterpret_cast<int32_t*>(smem + (LDS_SCENE ? 2 * n_nodes + n_leaves : 0)) + threadIdx.x;
+    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem + 2 * n_nodes + n_leaves) : w.node_km;
+    int32_t* stack = reinterpret_cast<int32_t*>(smem + (LDS_SCENE ? 2 * n_nodes + n_leaves + (n_nodes + 1) / 2 : 0)) +
+                     threadIdx.x;
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
     const RayPre rp{T.inv, T.fast != 0};
+    uint32_t db[DB_SHADE_CALLS] = {};
+    if (STATS) db[DB_TRAV_CALLS] = 1;
     for (;;) {
         const unsigned long long tr = __ballot(T.phase == PH_TRACE);
         if (tr == 0) break;
         if (__popcll(tr) < (unsigned)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
+        if (STATS) {
+            const unsigned long long nm = __ballot(T.phase == PH_TRACE && T.node >= 0);
+            const unsigned long long lm = tr & ~nm;
+            db[DB_ITERS]++;
+            db[DB_NODE_ITERS] += nm != 0;
+            db[DB_LEAF_ITERS] += lm != 0;
+            db[DB_NODE_LANES] += (uint32_t)__popcll(nm);
+            db[DB_LEAF_LANES] += (uint32_t)__popcll(lm);
+            db[DB_ALIVE_LANES] += (uint32_t)__popcll(__ballot(1));
+            db[DB_WAIT_LANES] += (uint32_t)__popcll(__ballot(T.phase == PH_SHADE));
+        }
         if (T.phase == PH_TRACE) {
             bool next_set = false;  // T.node already holds the next item to visit
             if (T.node >= 0) {
                 if (STATS) st.c[ST_NODES]++;
                 const float4 na = nodes_a[T.node];
                 const float4 nb = nodes_b[T.node];
-                if (node_pass(na, nb, T.ray, rp, 0.001f, T.te)) {
+                const float2 km = nkm[T.node];
+                if (node_pass(na, nb, km, T.ray, rp, 0.001f, T.te)) {
                     const int32_t lbits = __float_as_int(nb.z);
                     const int32_t left = lbits >> 2;
                     const int axis = lbits & 3;
@@ -895,6 +944,13 @@ __device__ __noinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int
                 if (sph.w == sph.w) {  // a plain sphere leaf (only reached as the root or via the stack)
                     if (STATS) st.c[ST_T_SPHERE]++;
                     sphere_leaf(sph, leaf, T.ray, T.te, T.found);
+                } else if (__float_as_int(sph.x) == 1) {  // a plain triangle
+                    if (STATS) st.c[ST_T_TRI]++;
+                    float t;
+                    if (tri_test(load_tri(w, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) {
+                        T.te = t;
+                        T.found = leaf;
+                    }
                 } else {
                     float t;
                     if (leaf_t<STATS>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) {
@@ -910,6 +966,10 @@ __device__ __noinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int
         }
     }
     if (STATS) {
+        const unsigned long long act = __ballot(1);
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)act) - 1)
+            for (int i = 0; i < DB_SHADE_CALLS; ++i)
+                if (db[i]) atomicAdd(&dbg[i], (unsigned long long)db[i]);
         T.n_nodes = st.c[ST_NODES];
         T.n_sph_rect = st.c[ST_T_SPHERE] | (st.c[ST_T_RECT] << 16);
         T.n_box_tri = st.c[ST_T_BOX] | (st.c[ST_T_TRI] << 16);
@@ -919,7 +979,8 @@ __device__ __noinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int
 
 template <bool STATS, bool LDS_SCENE>
 __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
-    // LDS: [scene: nodes (2 float4 each) + leaf records (1 float4 each)] [stack: depth x BLOCK]
+    // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
+    // per node)] [stack: depth x BLOCK]
     const DWorld& w = A.w;
     if (LDS_SCENE) {
         for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) {
@@ -927,6 +988,8 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
             smem[A.node_count + i] = w.node_b[i];
         }
         for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
+        float2* km = reinterpret_cast<float2*>(smem + 2 * A.node_count + A.leaf_count);
+        for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = w.node_km[i];
         __syncthreads();
     }
     Stats st;
@@ -935,13 +998,13 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
     const int lane = threadIdx.x & 63;
     const int per_tile = A.tile_w * A.tile_h;
 
-    // Per-lane state machine.  Pixels come from a queue in tile order (wave-aggregated
-    // atomics); each lane iterates its pixel's samples in order (the per-pixel f32 sum is the
-    // reference's sequential .sum(), rendering.rs:172-179).
+    // Per-lane state machine.  Work items (a slot and a run of `chunk` consecutive samples) come
+    // from a queue (wave-aggregated atomics), chunk-major so that a wave's lanes share a tile;
+    // each finished sample's colour is stored and accumulate_kernel adds them per pixel in
+    // sample order (the reference's sequential .sum(), rendering.rs:172-179).
     uint32_t pix = 0, slot = 0;
     float fx = 0.0f, fy = 0.0f;
-    V3 sum = v3(0.0f, 0.0f, 0.0f);
-    uint32_t sample = 0;
+    uint32_t sample = 0, sample_end = 0;
     V3 pdir = v3(0.0f, 0.0f, 0.0f), att = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
     int32_t depth = 0;
     Trav T;
@@ -975,16 +1038,18 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
             const unsigned long long m = __ballot(T.phase == PH_PIXEL);
             if (m == 0) break;
             const int leader = __ffsll((long long)m) - 1;
-            unsigned int base = 0;
-            if (lane == leader) base = atomicAdd(A.queue, (unsigned int)__popcll(m));
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
             base = __shfl(base, leader);
             if (T.phase == PH_PIXEL) {
                 const unsigned long long below = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
-                const uint32_t c = base + (uint32_t)__popcll(below);
-                if (c >= A.total) {
+                const uint64_t item = base + (uint64_t)__popcll(below);
+                if (item >= A.items) {
                     out_of_work = true;
                     T.phase = PH_TRACE;  // leaves the loops below
                 } else {
+                    const uint32_t ck = (uint32_t)(item / A.total);
+                    const uint32_t c = (uint32_t)(item - (uint64_t)ck * A.total);
                     const int32_t lt = (int32_t)(c / (uint32_t)per_tile);
                     const int32_t it = (int32_t)(c % (uint32_t)per_tile);
                     const int32_t tile = A.part_index + lt * A.part_count;
@@ -995,8 +1060,8 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
                         pix = (uint32_t)(py * A.width + px);
                         fx = (float)px * A.sx;  // size2i.rs:52-55
                         fy = (float)py * A.sy;
-                        sum = v3(0.0f, 0.0f, 0.0f);
-                        sample = 0;
+                        sample = A.s_begin + ck * A.chunk;
+                        sample_end = min(sample + A.chunk, A.s_end);
                         start_sample();
                         T.phase = PH_TRACE;
                     }
@@ -1019,7 +1084,8 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
         }
 
         // 3. traversal (hittable.rs:429-473)
-        T = traverse<STATS, LDS_SCENE>(A.wdev, T, A.trace_min, A.node_count, A.leaf_count);
+        T = traverse<STATS, LDS_SCENE>(A.wdev, T, A.trace_min, A.node_count, A.leaf_count,
+                                       STATS ? A.stats + ST_COUNT : nullptr);
         if (STATS) {
             st.c[ST_NODES] += T.n_nodes;
             st.c[ST_T_SPHERE] += T.n_sph_rect & 0xFFFFu;
@@ -1029,6 +1095,13 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
         }
 
         // 4. shade the lanes whose traversal finished (rendering.rs:19-71)
+        if (STATS) {
+            const unsigned long long sm = __ballot(T.phase == PH_SHADE);
+            if (sm && lane == __ffsll((long long)__ballot(1)) - 1) {
+                atomicAdd(&A.stats[ST_COUNT + DB_SHADE_CALLS], 1ull);
+                atomicAdd(&A.stats[ST_COUNT + DB_SHADE_LANES], (unsigned long long)__popcll(sm));
+            }
+        }
         if (T.phase == PH_SHADE) {
             if (STATS && T.found >= 0) {
                 st.c[ST_H_SPHERE + w.leaf_info[T.found].x]++;
@@ -1049,20 +1122,14 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
             if (STATS) st.c[ST_TEXEL] += so.texels;
             T.phase = PH_TRACE;
             if (so.done) {
-                sum = add(sum, so.color);
+                float* o = A.colors + ((uint64_t)(sample - A.s_begin) * A.total + slot) * 3;
+                o[0] = so.color.x;
+                o[1] = so.color.y;
+                o[2] = so.color.z;
                 if (STATS) st.c[ST_SAMPLES]++;
                 ++sample;
-                if (sample >= A.spp) {
-                    // rendering.rs:179: sum / spp; merge_planes with one plane multiplies by 1.0
-                    const V3 pixel = divs(sum, (float)A.spp);
-                    float* o = (A.layout == RTW_LAYOUT_TILES) ? A.out + (int64_t)slot * 3 : A.out + (int64_t)pix * 3;
-                    o[0] = pixel.x;
-                    o[1] = pixel.y;
-                    o[2] = pixel.z;
-                    T.phase = PH_PIXEL;
-                } else {
-                    start_sample();
-                }
+                if (sample >= sample_end) T.phase = PH_PIXEL;
+                else start_sample();
             } else {
                 fresh = true;  // the scattered ray continues the path
             }
@@ -1071,6 +1138,38 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
     if (STATS) {
         for (int i = 0; i < ST_COUNT; ++i)
             if (st.c[i]) atomicAdd(&A.stats[i], (unsigned long long)st.c[i]);
+    }
+}
+
+// Per slot: sum += colour of each sample of this launch, in sample order (the running sum of
+// earlier launches is carried in `running`); the last launch writes sum / spp (rendering.rs:179;
+// merge_planes with one plane multiplies by 1.0).
+__global__ void accumulate_kernel(const float* __restrict__ colors, uint32_t n_samples, uint32_t total,
+                                  float* __restrict__ running, int first, int last, uint32_t spp, float* out,
+                                  int layout, int32_t width, int32_t height, int32_t tile_w, int32_t tile_h,
+                                  int32_t tiles_x, int32_t part_index, int32_t part_count) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= total) return;
+    const int32_t per_tile = tile_w * tile_h;
+    const int32_t tile = part_index + (int32_t)(slot / (uint32_t)per_tile) * part_count;
+    const int32_t it = (int32_t)(slot % (uint32_t)per_tile);
+    const int32_t px = (tile % tiles_x) * tile_w + it % tile_w;
+    const int32_t py = (tile / tiles_x) * tile_h + it / tile_w;
+    if (px >= width || py >= height) return;  // padding slot of an edge tile
+    V3 sum = first ? v3(0.0f, 0.0f, 0.0f) : v3(running[3 * (size_t)slot], running[3 * (size_t)slot + 1],
+                                                running[3 * (size_t)slot + 2]);
+    const float* c = colors + 3 * (size_t)slot;
+    for (uint32_t s = 0; s < n_samples; ++s, c += 3 * (size_t)total) sum = add(sum, v3(c[0], c[1], c[2]));
+    if (last) {
+        const V3 pixel = divs(sum, (float)spp);
+        float* o = (layout == RTW_LAYOUT_TILES) ? out + 3 * (size_t)slot : out + 3 * ((size_t)py * width + px);
+        o[0] = pixel.x;
+        o[1] = pixel.y;
+        o[2] = pixel.z;
+    } else {
+        running[3 * (size_t)slot] = sum.x;
+        running[3 * (size_t)slot + 1] = sum.y;
+        running[3 * (size_t)slot + 2] = sum.z;
     }
 }
 
@@ -1226,7 +1325,11 @@ int check_world(const rtw_world* w, int* depth_out) {
 struct rtw_gpu_world {
     int device = 0;
     void* arena = nullptr;
-    unsigned int* queue = nullptr;  // pixel work counter (one render at a time per world)
+    unsigned long long* queue = nullptr;  // work-item counter (one render at a time per world)
+    float* colors = nullptr;   // per-sample colours of one launch (grown on demand)
+    size_t colors_bytes = 0;
+    float* running = nullptr;  // per-slot running sums between launches of one frame
+    size_t running_bytes = 0;
     DWorld w{};
     const DWorld* wdev = nullptr;
     int32_t node_count = 0, leaf_count = 0, depth = 1;
@@ -1264,6 +1367,14 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     }
     const size_t o_na = L.push(na.data(), na.size() * sizeof(float4));
     const size_t o_nb = L.push(nb.data(), nb.size() * sizeof(float4));
+    // proximity-cull constants (rtw_cull.h); RTW_NO_CULL=1 in the environment disables the cull
+    // (every node k = +inf: the reference traversal alone), for audits
+    std::vector<float> km((size_t)std::max(1, w->node_count) * 2, 0.0f);
+    {
+        const char* nc = std::getenv("RTW_NO_CULL");
+        rtw_cull_prepare(w, km.data(), nc && nc[0] && nc[0] != '0');
+    }
+    const size_t o_km = L.push(km.data(), km.size() * sizeof(float));
     // leaf records for the traversal: plain spheres inline, everything else tagged NaN
     std::vector<float4> lf((size_t)w->leaf_count);
     for (int i = 0; i < w->leaf_count; ++i) {
@@ -1272,7 +1383,9 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
             const rtw_sphere& sp = w->spheres[l.geom_index];
             lf[(size_t)i] = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius);
         } else {
-            lf[(size_t)i] = make_float4(0.0f, 0.0f, 0.0f, ibits(0x7FC00000));
+            // w = NaN: not a plain sphere; x = 1 tags a plain triangle (index in y)
+            const bool tri = l.geom_kind == RTW_GEOM_TRIANGLE && l.flags == 0;
+            lf[(size_t)i] = make_float4(ibits(tri ? 1 : 0), ibits(l.geom_index), 0.0f, ibits(0x7FC00000));
         }
     }
     const size_t o_lf = L.push(lf.data(), lf.size() * sizeof(float4));
@@ -1306,13 +1419,16 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         bx[2 * (size_t)i] = make_float4(b.min[0], b.min[1], b.min[2], b.max[0]);
         bx[2 * (size_t)i + 1] = make_float4(b.max[1], b.max[2], 0.0f, 0.0f);
     }
-    std::vector<float4> tp((size_t)w->triangle_count * 3), ta((size_t)w->triangle_count * 4);
+    std::vector<float4> tp((size_t)w->triangle_count * 4), ta((size_t)w->triangle_count * 4);
     for (int i = 0; i < w->triangle_count; ++i) {
         const rtw_triangle& t = w->triangles[i];
         const float (*p)[3] = t.positions;
-        tp[3 * (size_t)i] = make_float4(p[0][0], p[0][1], p[0][2], p[1][0]);
-        tp[3 * (size_t)i + 1] = make_float4(p[1][1], p[1][2], p[2][0], p[2][1]);
-        tp[3 * (size_t)i + 2] = make_float4(p[2][2], 0.0f, 0.0f, 0.0f);
+        const TriFast f = tri_prepare(v3(p[0][0], p[0][1], p[0][2]), v3(p[1][0], p[1][1], p[1][2]),
+                                      v3(p[2][0], p[2][1], p[2][2]));
+        tp[4 * (size_t)i] = make_float4(f.p0.x, f.p0.y, f.p0.z, f.n.x);
+        tp[4 * (size_t)i + 1] = make_float4(f.n.y, f.n.z, f.vt1.x, f.vt1.y);
+        tp[4 * (size_t)i + 2] = make_float4(f.vt1.z, f.den1, f.vt2.x, f.vt2.y);
+        tp[4 * (size_t)i + 3] = make_float4(f.vt2.z, f.den2, 0.0f, 0.0f);
         const float (*n)[3] = t.normals;
         const float (*u)[2] = t.uvs;
         ta[4 * (size_t)i] = make_float4(n[0][0], n[0][1], n[0][2], n[1][0]);
@@ -1393,13 +1509,14 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     DWorld& d = g->w;
     d.node_a = (const float4*)(base + o_na);
     d.node_b = (const float4*)(base + o_nb);
+    d.node_km = (const float2*)(base + o_km);
     d.leaf_fast = (const float4*)(base + o_lf);
     d.leaf_info = (const int4*)(base + o_li);
     d.leaf_xf = (const float4*)(base + o_lx);
     d.spheres = (const float4*)(base + o_sp);
     d.rects = (const float4*)(base + o_rc);
     d.boxes = (const float4*)(base + o_bx);
-    d.tri_pos = (const float4*)(base + o_tp);
+    d.tri_fast = (const float4*)(base + o_tp);
     d.tri_attr = (const float4*)(base + o_ta);
     d.materials = (const int4*)(base + o_mt);
     d.textures = (const int4*)(base + o_tx);
@@ -1438,6 +1555,8 @@ extern "C" RTW_API int rtw_world_release(rtw_gpu_world* g) {
     (void)hipSetDevice(g->device);
     if (g->arena) (void)hipFree(g->arena);
     if (g->queue) (void)hipFree(g->queue);
+    if (g->colors) (void)hipFree(g->colors);
+    if (g->running) (void)hipFree(g->running);
     delete g;
     return RTW_OK;
 }
@@ -1490,7 +1609,7 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
 // Launch the persistent render kernel: zero the pixel queue, stage the scene in LDS when it
 // fits, size the grid to the resident block count.
 int launch_render(rtw_gpu_world* g, KArgs& A, bool stats, hipStream_t stream) {
-    const size_t scene_bytes = (size_t)(2 * g->node_count + g->leaf_count) * sizeof(float4);
+    const size_t scene_bytes = (size_t)(2 * g->node_count + g->leaf_count + (g->node_count + 1) / 2) * sizeof(float4);
     const bool lds_scene = scene_bytes <= RTW_LDS_SCENE_MAX;
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
     const size_t lds = (lds_scene ? scene_bytes : 0) + stack_bytes;
@@ -1501,9 +1620,9 @@ int launch_render(rtw_gpu_world* g, KArgs& A, bool stats, hipStream_t stream) {
     int per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, RTW_BLOCK, lds));
     if (per_cu < 1) return rtw::fail(RTW_ERR_UNSUPPORTED, "render kernel does not fit on a CU");
-    const int64_t want = ((int64_t)A.total + RTW_BLOCK - 1) / RTW_BLOCK;
+    const int64_t want = (int64_t)((A.items + RTW_BLOCK - 1) / RTW_BLOCK);
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per_cu * g->cus));
-    HIP_TRY(hipMemsetAsync(g->queue, 0, sizeof(unsigned int), stream));
+    HIP_TRY(hipMemsetAsync(g->queue, 0, sizeof(unsigned long long), stream));
     if (stats) {
         if (lds_scene) hipLaunchKernelGGL((render_kernel<true, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
         else hipLaunchKernelGGL((render_kernel<true, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
@@ -1512,6 +1631,57 @@ int launch_render(rtw_gpu_world* g, KArgs& A, bool stats, hipStream_t stream) {
         else hipLaunchKernelGGL((render_kernel<false, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
     }
     HIP_TRY(hipGetLastError());
+    return RTW_OK;
+}
+
+size_t env_size(const char* name, size_t dflt) {
+    const char* e = std::getenv(name);
+    if (!e || !e[0]) return dflt;
+    const long long v = std::atoll(e);
+    return v > 0 ? (size_t)v : dflt;
+}
+
+int grow(void** buf, size_t* have, size_t need) {
+    if (*have >= need) return RTW_OK;
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    const hipError_t e = hipMalloc(buf, need);
+    if (e != hipSuccess) return rtw::fail(RTW_ERR_OUT_OF_MEMORY, std::string("hipMalloc: ") + hipGetErrorString(e));
+    *have = need;
+    return RTW_OK;
+}
+
+// One frame: launches of at most RTW_SAMPLE_BUFFER_BYTES (default 16 GiB) of per-sample colours,
+// each followed by the in-order accumulation; work items of RTW_CHUNK (default 8) samples.
+int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream) {
+    if (A.total == 0) return RTW_OK;
+    const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 8));
+    const size_t budget = env_size("RTW_SAMPLE_BUFFER_BYTES", (size_t)16 << 30);
+    const size_t per_sample = (size_t)A.total * 3 * sizeof(float);
+    uint64_t per_launch = std::max<uint64_t>(chunk, (budget / per_sample) / chunk * chunk);
+    per_launch = std::min<uint64_t>(per_launch, A.spp);
+    int rc = grow((void**)&g->colors, &g->colors_bytes, per_sample * per_launch);
+    if (rc != RTW_OK) return rc;
+    if (per_launch < A.spp) {
+        rc = grow((void**)&g->running, &g->running_bytes, per_sample);
+        if (rc != RTW_OK) return rc;
+    }
+    A.colors = g->colors;
+    A.chunk = chunk;
+    for (uint32_t s0 = 0; s0 < A.spp; s0 += (uint32_t)per_launch) {
+        const uint32_t s1 = (uint32_t)std::min<uint64_t>(A.spp, s0 + per_launch);
+        A.s_begin = s0;
+        A.s_end = s1;
+        A.items = (uint64_t)A.total * ((s1 - s0 + chunk - 1) / chunk);
+        rc = launch_render(g, A, stats, stream);
+        if (rc != RTW_OK) return rc;
+        const unsigned blocks = (A.total + 255) / 256;
+        hipLaunchKernelGGL(accumulate_kernel, dim3(blocks), dim3(256), 0, stream, (const float*)g->colors, s1 - s0,
+                           A.total, g->running, s0 == 0 ? 1 : 0, s1 == A.spp ? 1 : 0, A.spp, out, A.layout, A.width,
+                           A.height, A.tile_w, A.tile_h, A.tiles_x, A.part_index, A.part_count);
+        HIP_TRY(hipGetLastError());
+    }
     return RTW_OK;
 }
 
@@ -1537,11 +1707,11 @@ extern "C" RTW_API int rtw_render_device(rtw_gpu_world* g, const rtw_render_para
     if (!d_out) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null output");
     A.out = d_out;
     HIP_TRY(hipSetDevice(g->device));
-    if (A.total == 0) return RTW_OK;
-    return launch_render(g, A, false, (hipStream_t)stream);
+    return render_frame(g, A, false, d_out, (hipStream_t)stream);
 }
 
-extern "C" RTW_API int rtw_render_collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s) {
+namespace {
+int collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s, uint64_t* dbg, int dbg_n) {
     KArgs A;
     const int v = make_args(g, p, A);
     if (v != RTW_OK) return v;
@@ -1550,20 +1720,22 @@ extern "C" RTW_API int rtw_render_collect_stats(rtw_gpu_world* g, const rtw_rend
     float* out = nullptr;
     unsigned long long* st = nullptr;
     HIP_TRY(hipMalloc(&out, (size_t)p->width * p->height * 3 * sizeof(float)));
-    HIP_TRY(hipMalloc(&st, ST_COUNT * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(st, 0, ST_COUNT * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&st, (ST_COUNT + DB_COUNT) * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(st, 0, (ST_COUNT + DB_COUNT) * sizeof(unsigned long long)));
     A.out = out;
     A.layout = RTW_LAYOUT_IMAGE;
     A.stats = st;
-    if (A.total > 0) {
-        const int rc = launch_render(g, A, true, 0);
+    {
+        const int rc = render_frame(g, A, true, out, 0);
         if (rc != RTW_OK) return rc;
     }
     HIP_TRY(hipDeviceSynchronize());
-    unsigned long long h[ST_COUNT];
+    unsigned long long h[ST_COUNT + DB_COUNT];
     HIP_TRY(hipMemcpy(h, st, sizeof(h), hipMemcpyDeviceToHost));
     (void)hipFree(out);
     (void)hipFree(st);
+    if (dbg)
+        for (int i = 0; i < dbg_n && i < DB_COUNT; ++i) dbg[i] = h[ST_COUNT + i];
     s->samples = h[ST_SAMPLES];
     s->rays = h[ST_RAYS];
     s->node_visits = h[ST_NODES];
@@ -1578,6 +1750,17 @@ extern "C" RTW_API int rtw_render_collect_stats(rtw_gpu_world* g, const rtw_rend
     s->material_reads = h[ST_MAT];
     s->texel_reads = h[ST_TEXEL];
     return RTW_OK;
+}
+}  // namespace
+
+extern "C" RTW_API int rtw_render_collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s) {
+    return collect_stats(g, p, s, nullptr, 0);
+}
+
+extern "C" RTW_API int rtw_render_debug_counters(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s,
+                                                 uint64_t* counters, int n) {
+    if (!counters || n < 0) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null counters");
+    return collect_stats(g, p, s, counters, n);
 }
 
 extern "C" RTW_API int rtw_render(const rtw_world* w, const rtw_render_params* p, int device, float* out_rgb) {

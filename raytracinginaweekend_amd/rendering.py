@@ -109,6 +109,16 @@ class DeviceWorld:
         check(lib().rtw_render_collect_stats(self._h, C.byref(params), C.byref(s)))
         return s.as_dict()
 
+    DEBUG_COUNTERS = ("trav_calls", "iters", "node_iters", "leaf_iters", "node_lanes", "leaf_lanes",
+                      "alive_lanes", "wait_lanes", "shade_calls", "shade_lanes")
+
+    def debug_counters(self, params: N.RenderParams) -> tuple[dict, dict]:
+        """(statistics, wave-level execution counters) of one counting-variant render."""
+        s = N.RenderStats()
+        c = (C.c_uint64 * len(self.DEBUG_COUNTERS))()
+        check(lib().rtw_render_debug_counters(self._h, C.byref(params), C.byref(s), c, len(c)))
+        return s.as_dict(), dict(zip(self.DEBUG_COUNTERS, list(c)))
+
 
 def partition_floats(params: N.RenderParams) -> int:
     n = C.c_int64()

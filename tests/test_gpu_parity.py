@@ -54,3 +54,16 @@ def test_shallow_depths(worlds, max_depth):
     gpu = R.render(size, 1, 4, max_depth, world, seed=5)
     ref = O.render(world, R.render_params(size, 4, max_depth, seed=5))
     assert_bit_identical(gpu, ref, f"depth {max_depth}")
+
+
+@pytest.mark.parametrize("chunk,buffer_bytes", [("1", None), ("3", "200000"), ("8", "50000"), ("64", None)])
+def test_work_item_split_is_bit_exact(worlds, chunk, buffer_bytes, monkeypatch):
+    """Work items of `chunk` samples and frames split over several launches (small colour buffer:
+    the running sum is carried between launches) give the oracle's bits."""
+    world = worlds("final_scene1")
+    monkeypatch.setenv("RTW_CHUNK", chunk)
+    if buffer_bytes:
+        monkeypatch.setenv("RTW_SAMPLE_BUFFER_BYTES", buffer_bytes)
+    p = R.render_params(R.Size2i(40, 24), 37, 50, seed=13)
+    gpu = R.render(R.Size2i(40, 24), 1, 37, 50, world, seed=13)
+    assert_bit_identical(gpu, O.render(world, p, O.RNG_CTR), f"chunk {chunk}")
