@@ -67,3 +67,17 @@ def test_work_item_split_is_bit_exact(worlds, chunk, buffer_bytes, monkeypatch):
     p = R.render_params(R.Size2i(40, 24), 37, 50, seed=13)
     gpu = R.render(R.Size2i(40, 24), 1, 37, 50, world, seed=13)
     assert_bit_identical(gpu, O.render(world, p, O.RNG_CTR), f"chunk {chunk}")
+
+
+@pytest.mark.parametrize("name", ["final_scene1", "suzanne", "cornell_box", "cornell_cube", "final_scene2",
+                                  "earth_mapped", "cornell_box_smoke"])
+def test_golden_frames(name):
+    """The committed golden frames (tests/golden/images.npz), bit for bit, through rtw_render."""
+    import os
+
+    from tests.golden.make_golden import IMAGES
+
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "images.npz"))
+    _, w, h, spp, depth, seed = next(c for c in IMAGES if c[0] == name)
+    gpu = R.render(R.Size2i(w, h), 1, spp, depth, R.demo_world(name), seed=seed)
+    assert_bit_identical(gpu, fx[name], name)
