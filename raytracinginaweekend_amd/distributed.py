@@ -1,15 +1,21 @@
-"""Multi-GPU frame rendering: interleaved tile partition + one RCCL gather.
+"""Multi-GPU frame rendering: interleaved tile partition + one collective gather.
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Rank r renders the
 tiles t with t % N == r of the frame into a compact tile buffer (RTW_LAYOUT_TILES); the buffers
-(padded to rank 0's size) are all-gathered and rank 0 scatters them into the image with
-rtw_untile_device.  Because the RNG stream is keyed by (seed, pixel, sample), the image is
-bit-identical for every N.  PyTorch is plumbing here: device memory, the stream and the
+(padded to rank 0's size, rtw_partition_floats) are all-gathered and rank 0 scatters them into
+the image (rtw_untile_device).  Because the RNG stream is keyed by (seed, pixel, sample), the
+image is bit-identical for every N.  PyTorch is plumbing here: device memory, the stream and the
 collective; the render itself is librtw.so's kernel.
+
+TileExchange holds the partition arithmetic and the gather/untile step for both device tensors
+(RCCL + the untile kernel) and host tensors (gloo + untile_host, the CPU mirror used by the
+world-size-2 tests).
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
+
+import numpy as np
 
 from . import _native as N
 from .rendering import DeviceWorld, Size2i, partition_floats, render_params, untile_device
@@ -25,11 +31,9 @@ class FrameSpec:
     tile: tuple[int, int] = (8, 8)
 
 
-def tile_slots(size: Size2i, tile: tuple[int, int], part: tuple[int, int]):
+def tile_slots(size: Size2i, tile: tuple[int, int], part: tuple[int, int]) -> np.ndarray:
     """Pixel index (or -1 for padding) of every slot of one partition's tile buffer (host-side
-    mirror of the kernel's layout, used by the CPU tests of the gather/untile logic)."""
-    import numpy as np
-
+    mirror of the kernel's layout: owned tiles t = idx, idx + pc, ... row-major inside)."""
     tw, th = tile
     tiles_x = -(-size.width // tw)
     n_tiles = tiles_x * -(-size.height // th)
@@ -39,6 +43,62 @@ def tile_slots(size: Size2i, tile: tuple[int, int], part: tuple[int, int]):
     px = (owned % tiles_x) * tw + j % tw
     py = (owned // tiles_x) * th + j // tw
     return np.where((px < size.width) & (py < size.height), py * size.width + px, -1).ravel()
+
+
+def pack_tiles(image: np.ndarray, size: Size2i, tile: tuple[int, int], part: tuple[int, int], stride: int) -> np.ndarray:
+    """A partition's tile buffer (RTW_LAYOUT_TILES, padded to `stride` floats) cut from a full
+    (H*W, 3) image: what the kernel writes for that partition."""
+    slots = tile_slots(size, tile, part)
+    buf = np.zeros(stride, np.float32)
+    v = buf[: len(slots) * 3].reshape(-1, 3)
+    ok = slots >= 0
+    v[ok] = image.reshape(-1, 3)[slots[ok]]
+    return buf
+
+
+def untile_host(gathered: np.ndarray, size: Size2i, tile: tuple[int, int], part_count: int, stride: int) -> np.ndarray:
+    """CPU mirror of untile_kernel (rtw_device.hip): the gathered buffers -> (H*W, 3) image."""
+    img = np.zeros((size.width * size.height, 3), np.float32)
+    for r in range(part_count):
+        slots = tile_slots(size, tile, (r, part_count))
+        src = gathered[r * stride: r * stride + len(slots) * 3].reshape(-1, 3)
+        ok = slots >= 0
+        img[slots[ok]] = src[ok]
+    return img
+
+
+class TileExchange:
+    """Partition arithmetic + the gather step of one frame for rank `rank` of `world_size`."""
+
+    def __init__(self, spec: FrameSpec, rank: int, world_size: int):
+        self.spec, self.rank, self.world_size = spec, rank, world_size
+        p0 = render_params(spec.size, 1, 1, tile=spec.tile, part=(0, world_size), layout=N.LAYOUT_TILES)
+        self.stride = partition_floats(p0)  # rank 0 owns the most tiles
+        self.params = render_params(spec.size, spec.samples_per_pixel, spec.max_depth, seed=spec.seed,
+                                    tile=spec.tile, part=(rank, world_size),
+                                    layout=N.LAYOUT_TILES if world_size > 1 else N.LAYOUT_IMAGE)
+
+    def pixels_this_rank(self) -> int:
+        return int((tile_slots(self.spec.size, self.spec.tile, (self.rank, self.world_size)) >= 0).sum())
+
+    def gather(self, tiles, gathered) -> None:
+        """All-gather the padded tile buffers (RCCL for device tensors, gloo for host ones)."""
+        import torch.distributed as dist
+
+        if tiles.is_cuda:
+            dist.all_gather_into_tensor(gathered, tiles)
+        else:
+            dist.all_gather(list(gathered.view(self.world_size, -1).unbind(0)), tiles)
+
+    def untile(self, gathered, image, stream_ptr: int | None = None) -> None:
+        """Rank 0: scatter the gathered buffers into the (W*H*3) image."""
+        if gathered.is_cuda:
+            untile_device(self.params, gathered.data_ptr(), self.stride, image.data_ptr(), stream_ptr)
+        else:
+            import torch
+
+            img = untile_host(gathered.numpy(), self.spec.size, self.spec.tile, self.world_size, self.stride)
+            image.copy_(torch.from_numpy(img.ravel()))
 
 
 class FrameRenderer:
@@ -51,11 +111,9 @@ class FrameRenderer:
         self.spec, self.rank, self.world_size = spec, rank, world_size
         self.dev = torch.device("cuda", device)
         self.dworld = DeviceWorld(world, device)
-        layout = N.LAYOUT_TILES if world_size > 1 else N.LAYOUT_IMAGE
-        self.params = render_params(spec.size, spec.samples_per_pixel, spec.max_depth, seed=spec.seed,
-                                    tile=spec.tile, part=(rank, world_size), layout=layout)
-        p0 = render_params(spec.size, 1, 1, tile=spec.tile, part=(0, world_size), layout=N.LAYOUT_TILES)
-        self.stride = partition_floats(p0)  # rank 0 owns the most tiles
+        self.xchg = TileExchange(spec, rank, world_size)
+        self.params = self.xchg.params
+        self.stride = self.xchg.stride
         npix = spec.size.width * spec.size.height
         self.image = torch.zeros(npix * 3, dtype=torch.float32, device=self.dev)
         if world_size > 1:
@@ -74,11 +132,9 @@ class FrameRenderer:
         """One RCCL all-gather of the tile buffers + the untile on rank 0."""
         if self.world_size == 1:
             return
-        import torch.distributed as dist
-
-        dist.all_gather_into_tensor(self.gathered, self.tiles)
+        self.xchg.gather(self.tiles, self.gathered)
         if self.rank == 0:
-            untile_device(self.params, self.gathered.data_ptr(), self.stride, self.image.data_ptr(), self.stream_ptr())
+            self.xchg.untile(self.gathered, self.image, self.stream_ptr())
 
     def render_frame(self):
         self.launch()
@@ -86,4 +142,4 @@ class FrameRenderer:
         return self.image
 
     def pixels_this_rank(self) -> int:
-        return int((tile_slots(self.spec.size, self.spec.tile, (self.rank, self.world_size)) >= 0).sum())
+        return self.xchg.pixels_this_rank()

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+try:  # first, so that librtw.so binds to the HIP runtime torch ships (one runtime per process)
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
