@@ -703,7 +703,7 @@ struct ShadeOut {
 };
 
 template <bool STATS>
-__device__ __noinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t mode, Path P, int32_t found, float te,
+__device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t mode, Path P, int32_t found, float te,
                                        V3 pdir) {
     const DWorld& w = *wp;
     Stats st;
@@ -862,7 +862,7 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 }
 
 template <bool STATS, bool LDS_SCENE>
-__device__ __noinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
+__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
                                       int32_t n_leaves, unsigned long long* dbg) {
     const DWorld& w = *wp;
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
