@@ -4,7 +4,7 @@
  * evaluate the identical per-node test.  Host-only C99/C++.
  *
  * km[2 n] = k, km[2 n + 1] = m for node n; the per-(ray, node) margin is
- *   delta = k D^2 + 64u D + m          (u = 2^-24, D = rtw_cull_axis_d summed over the axes)
+ *   delta = k D^2 + 64u D + m      (u = 2^-24, D = sum_i |min_i - o_i| + |max_i - o_i|)
  * k and m are the maxima over the leaves below n of
  *   plain sphere (SurfaceGeometry, no Transformation/Animation, hittable.rs:212-247; sphere
  *     test sphere_geometry.rs:21-59):  k = 64u / r,  m = 8u (max_i |c_i| + r)

@@ -478,7 +478,7 @@ RTW_HD float rtw_sinf(float x) {
 /* would accept a root in [ts, te), so the closest hit, its tie-breaking and every RNG draw     */
 /* are those of the reference traversal (argument and error bounds: DESIGN.md "Proximity       */
 /* cull"; node constants k, m: rtw_cull.h).                                                     */
-/*   per (ray, node): D = sum_i max(|min_i - o_i|, |max_i - o_i|) >= |o - x| for every x in    */
+/*   per (ray, node): D = sum_i (|min_i - o_i| + |max_i - o_i|) >= |o - x| for every x in     */
 /*   the box; delta = k D^2 + 64u D + m bounds how far outside the box a computed hit point of  */
 /*   a leaf below can lie (plus the quotient roundings); the node passes when the ray segment   */
 /*   [ts, te] meets the box grown by delta, reusing hit_cond's slab quotients.                  */

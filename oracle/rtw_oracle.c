@@ -381,7 +381,7 @@ static int cull_pass(const float* km, int32_t n, const rtw_bvh_node* nd, const R
     for (int i = 0; i < 3; ++i) {
         const float a = nd->min[i] - r->origin.e[i];
         const float b = nd->max[i] - r->origin.e[i];
-        d += fmaxf(fabsf(a), fabsf(b));
+        d += fabsf(a) + fabsf(b);
         const float qa = a / r->dir.e[i], qb = b / r->dir.e[i];
         t0[i] = (qa < qb) ? qa : qb;
         t1[i] = (qa < qb) ? qb : qa;

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librtw.so")
+LIB_PATH = os.environ.get("RTW_LIBRARY") or os.path.join(_HERE, "librtw.so")  # override: experiments only
 
 RTW_OK = 0
 RTW_ERR_INVALID_ARGUMENT = 1

@@ -27,10 +27,16 @@
 #include "../../include/rtw_cull.h"
 #include "rtw_common.h"
 
+#ifndef RTW_BLOCK
 #define RTW_BLOCK 512   // 8 waves; 2 blocks per CU at <= 128 VGPRs -> 4 waves per SIMD
+#endif
+#ifndef RTW_MIN_WAVES_PER_SIMD
 #define RTW_MIN_WAVES_PER_SIMD 4
+#endif
 #define RTW_STACK 32    // per-lane traversal stack (LDS), >= the BVH depth (checked at upload)
+#ifndef RTW_LDS_SCENE_MAX
 #define RTW_LDS_SCENE_MAX (96 * 1024)  // nodes + leaf records staged in LDS when they fit
+#endif
 
 namespace {
 
@@ -159,7 +165,8 @@ enum {
 // after the ST_COUNT statistics: traversal calls / loop iterations / iterations that ran the node
 // resp. leaf path / lanes stepping a node resp. a leaf / shade calls / lanes shading
 enum { DB_TRAV_CALLS, DB_ITERS, DB_NODE_ITERS, DB_LEAF_ITERS, DB_NODE_LANES, DB_LEAF_LANES, DB_ALIVE_LANES,
-       DB_WAIT_LANES, DB_SHADE_CALLS, DB_SHADE_LANES, DB_COUNT };
+       DB_WAIT_LANES, DB_PASS_LANES, DB_SN_ITERS, DB_SN_LANES, DB_SF_ITERS, DB_SF_LANES, DB_SHADE_CALLS,
+       DB_SHADE_LANES, DB_COUNT };
 struct Stats {
     uint32_t c[ST_COUNT];
 };
@@ -521,9 +528,9 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
     const float lo = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fabsf(a0), __builtin_fabsf(b0)),
                                                      __builtin_fminf(__builtin_fabsf(a1), __builtin_fabsf(b1))),
                                      __builtin_fminf(__builtin_fabsf(a2), __builtin_fabsf(b2)));
-    const float dsum = (__builtin_fmaxf(__builtin_fabsf(a0), __builtin_fabsf(b0)) +
-                        __builtin_fmaxf(__builtin_fabsf(a1), __builtin_fabsf(b1))) +
-                       __builtin_fmaxf(__builtin_fabsf(a2), __builtin_fabsf(b2));
+    // D = sum_i |a_i| + |b_i| (>= sum_i max(|a_i|, |b_i|) >= |o - x|; abs-modifier adds, no max)
+    const float dsum = ((__builtin_fabsf(a0) + __builtin_fabsf(b0)) + (__builtin_fabsf(a1) + __builtin_fabsf(b1))) +
+                       (__builtin_fabsf(a2) + __builtin_fabsf(b2));
     // |a| <= 2^32 always: rtw_world_upload bounds every coordinate by 2^30 (check_world)
     float qa0, qb0, qa1, qb1, qa2, qb2;
     if (__builtin_expect(rp.fast && lo >= RTW_MK_AMIN, 1)) {
@@ -541,14 +548,23 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
         qa2 = a2 / r.d.z;
         qb2 = b2 / r.d.z;
     }
-    // all three axes evaluated (no short-circuit): one predicate instead of three nested branches
-    const int hit_cond = (int)(te > ts) & (int)axis_pass(qa0, qb0, ts, te) & (int)axis_pass(qa1, qb1, ts, te) &
-                         (int)axis_pass(qa2, qb2, ts, te);
+    // minmax per axis (math.rs:35-41: `a < b` else swapped)
+    const bool l0 = qa0 < qb0, l1 = qa1 < qb1, l2 = qa2 < qb2;
+    const float t00 = l0 ? qa0 : qb0, t10 = l0 ? qb0 : qa0;
+    const float t01 = l1 ? qa1 : qb1, t11 = l1 ? qb1 : qa1;
+    const float t02 = l2 ? qa2 : qb2, t12 = l2 ? qb2 : qa2;
+    // hit_cond over the three axes at once: AND_i axis_pass(...) ==
+    //   te > ts && !(min_i t1_i <= ts) && !(te <= max_i t0_i) && AND_i qa_i != qb_i
+    // (min/max drop NaN operands, exactly the axes whose comparison is vacuously true)
+    const float t1min = __builtin_fminf(__builtin_fminf(t10, t11), t12);
+    const float t0max = __builtin_fmaxf(__builtin_fmaxf(t00, t01), t02);
+    const int hit_cond = (int)(te > ts) & (int)!(t1min <= ts) & (int)!(te <= t0max) & (int)(qa0 != qb0) &
+                         (int)(qa1 != qb1) & (int)(qa2 != qb2);
     const float delta = rtw_cull_delta(km.x, km.y, dsum);
     float clo = ts, chi = te;
-    rtw_cull_axis(qa0 < qb0 ? qa0 : qb0, qa0 < qb0 ? qb0 : qa0, delta * __builtin_fabsf(rp.inv.x), &clo, &chi);
-    rtw_cull_axis(qa1 < qb1 ? qa1 : qb1, qa1 < qb1 ? qb1 : qa1, delta * __builtin_fabsf(rp.inv.y), &clo, &chi);
-    rtw_cull_axis(qa2 < qb2 ? qa2 : qb2, qa2 < qb2 ? qb2 : qa2, delta * __builtin_fabsf(rp.inv.z), &clo, &chi);
+    rtw_cull_axis(t00, t10, delta * __builtin_fabsf(rp.inv.x), &clo, &chi);
+    rtw_cull_axis(t01, t11, delta * __builtin_fabsf(rp.inv.y), &clo, &chi);
+    rtw_cull_axis(t02, t12, delta * __builtin_fabsf(rp.inv.z), &clo, &chi);
     return hit_cond & (int)(clo <= chi);
 }
 
@@ -876,100 +892,86 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
     const RayPre rp{T.inv, T.fast != 0};
+    // execution counters, summed over lanes at the end: wave-level events are counted by the
+    // first active lane of the wave (or of the branch) only
     uint32_t db[DB_SHADE_CALLS] = {};
-    if (STATS) db[DB_TRAV_CALLS] = 1;
+    const bool lead0 = (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
+    if (STATS && lead0) db[DB_TRAV_CALLS] = 1;
+    // Each iteration a lane first tests the leaf it stands on, if any (popping the next item),
+    // then tests the node it stands on, if any (pushing the far child, moving to the near one):
+    // one leaf body and one node body per iteration, both in the reference's DFS order with the
+    // current t_range.  A lane reaching a leaf child tests it at the start of the next iteration.
     for (;;) {
         const unsigned long long tr = __ballot(T.phase == PH_TRACE);
         if (tr == 0) break;
         if (__popcll(tr) < (unsigned)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
         if (STATS) {
-            const unsigned long long nm = __ballot(T.phase == PH_TRACE && T.node >= 0);
-            const unsigned long long lm = tr & ~nm;
-            db[DB_ITERS]++;
-            db[DB_NODE_ITERS] += nm != 0;
-            db[DB_LEAF_ITERS] += lm != 0;
-            db[DB_NODE_LANES] += (uint32_t)__popcll(nm);
-            db[DB_LEAF_LANES] += (uint32_t)__popcll(lm);
-            db[DB_ALIVE_LANES] += (uint32_t)__popcll(__ballot(1));
-            db[DB_WAIT_LANES] += (uint32_t)__popcll(__ballot(T.phase == PH_SHADE));
+            const unsigned long long lm = __ballot(T.phase == PH_TRACE && T.node < 0);
+            const uint32_t alive = (uint32_t)__popcll(__ballot(1));
+            const uint32_t waiting = (uint32_t)__popcll(__ballot(T.phase == PH_SHADE));
+            if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
+                db[DB_ITERS]++;
+                db[DB_LEAF_ITERS] += lm != 0;
+                db[DB_LEAF_LANES] += (uint32_t)__popcll(lm);
+                db[DB_ALIVE_LANES] += alive;
+                db[DB_WAIT_LANES] += waiting;
+            }
         }
-        if (T.phase == PH_TRACE) {
-            bool next_set = false;  // T.node already holds the next item to visit
-            if (T.node >= 0) {
-                if (STATS) st.c[ST_NODES]++;
-                const float4 na = nodes_a[T.node];
-                const float4 nb = nodes_b[T.node];
-                const float2 km = nkm[T.node];
-                if (node_pass(na, nb, km, T.ray, rp, 0.001f, T.te)) {
-                    const int32_t lbits = __float_as_int(nb.z);
-                    const int32_t left = lbits >> 2;
-                    const int axis = lbits & 3;
-                    const int32_t right = __float_as_int(nb.w);
-                    const bool fwd = comp(T.ray.d, axis) > 0.0f;
-                    const int32_t near = fwd ? left : right;
-                    const int32_t far = fwd ? right : left;
-                    // hit_index_list order: near subtree, then far.  A plain-sphere leaf child is
-                    // tested right here (same order, same t_range), saving a divergent iteration.
-                    float4 sn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                    bool near_fast = false;
-                    if (near < 0) {
-                        sn = fast[-1 - near];
-                        near_fast = sn.w == sn.w;
-                    }
-                    if (near_fast) {
-                        if (STATS) st.c[ST_T_SPHERE]++;
-                        sphere_leaf(sn, -1 - near, T.ray, T.te, T.found);
-                        bool far_fast = false;
-                        float4 sf = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        if (far < 0) {
-                            sf = fast[-1 - far];
-                            far_fast = sf.w == sf.w;
-                        }
-                        if (far_fast) {
-                            if (STATS) st.c[ST_T_SPHERE]++;
-                            sphere_leaf(sf, -1 - far, T.ray, T.te, T.found);
-                        } else {
-                            T.node = far;
-                            next_set = true;
-                        }
-                    } else {
-                        stack[(T.sp++) * RTW_BLOCK] = far;
-                        T.node = near;
-                        next_set = true;
-                    }
+        if (T.phase == PH_TRACE && T.node < 0) {
+            const int leaf = -1 - T.node;
+            const float4 sph = fast[leaf];
+            if (sph.w == sph.w) {  // a plain sphere
+                if (STATS) st.c[ST_T_SPHERE]++;
+                sphere_leaf(sph, leaf, T.ray, T.te, T.found);
+            } else if (__float_as_int(sph.x) == 1) {  // a plain triangle
+                if (STATS) st.c[ST_T_TRI]++;
+                float t;
+                if (tri_test(load_tri(w, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) {
+                    T.te = t;
+                    T.found = leaf;
                 }
             } else {
-                const int leaf = -1 - T.node;
-                const float4 sph = fast[leaf];
-                if (sph.w == sph.w) {  // a plain sphere leaf (only reached as the root or via the stack)
-                    if (STATS) st.c[ST_T_SPHERE]++;
-                    sphere_leaf(sph, leaf, T.ray, T.te, T.found);
-                } else if (__float_as_int(sph.x) == 1) {  // a plain triangle
-                    if (STATS) st.c[ST_T_TRI]++;
-                    float t;
-                    if (tri_test(load_tri(w, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) {
-                        T.te = t;
-                        T.found = leaf;
-                    }
-                } else {
-                    float t;
-                    if (leaf_t<STATS>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) {
-                        T.te = t;
-                        T.found = leaf;
-                    }
+                float t;
+                if (leaf_t<STATS>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) {
+                    T.te = t;
+                    T.found = leaf;
                 }
             }
-            if (!next_set) {
-                if (T.sp == 0) T.phase = PH_SHADE;
-                else T.node = stack[(--T.sp) * RTW_BLOCK];
+            if (T.sp == 0) T.phase = PH_SHADE;
+            else T.node = stack[(--T.sp) * RTW_BLOCK];
+        }
+        if (STATS) {
+            const unsigned long long nm = __ballot(T.phase == PH_TRACE && T.node >= 0);
+            if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
+                db[DB_NODE_ITERS] += nm != 0;
+                db[DB_NODE_LANES] += (uint32_t)__popcll(nm);
+            }
+        }
+        if (T.phase == PH_TRACE && T.node >= 0) {
+            if (STATS) st.c[ST_NODES]++;
+            const float4 na = nodes_a[T.node];
+            const float4 nb = nodes_b[T.node];
+            const float2 km = nkm[T.node];
+            if (node_pass(na, nb, km, T.ray, rp, 0.001f, T.te)) {
+                if (STATS) db[DB_PASS_LANES]++;
+                const int32_t lbits = __float_as_int(nb.z);
+                const int32_t left = lbits >> 2;
+                const int axis = lbits & 3;
+                const int32_t right = __float_as_int(nb.w);
+                const bool fwd = comp(T.ray.d, axis) > 0.0f;
+                // hit_index_list order: near subtree, then far
+                stack[(T.sp++) * RTW_BLOCK] = fwd ? right : left;
+                T.node = fwd ? left : right;
+            } else if (T.sp == 0) {
+                T.phase = PH_SHADE;
+            } else {
+                T.node = stack[(--T.sp) * RTW_BLOCK];
             }
         }
     }
     if (STATS) {
-        const unsigned long long act = __ballot(1);
-        if ((int)(threadIdx.x & 63) == __ffsll((long long)act) - 1)
-            for (int i = 0; i < DB_SHADE_CALLS; ++i)
-                if (db[i]) atomicAdd(&dbg[i], (unsigned long long)db[i]);
+        for (int i = 0; i < DB_SHADE_CALLS; ++i)
+            if (db[i]) atomicAdd(&dbg[i], (unsigned long long)db[i]);
         T.n_nodes = st.c[ST_NODES];
         T.n_sph_rect = st.c[ST_T_SPHERE] | (st.c[ST_T_RECT] << 16);
         T.n_box_tri = st.c[ST_T_BOX] | (st.c[ST_T_TRI] << 16);
@@ -1334,6 +1336,7 @@ struct rtw_gpu_world {
     const DWorld* wdev = nullptr;
     int32_t node_count = 0, leaf_count = 0, depth = 1;
     int cus = 0;
+    int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
 };
 
 extern "C" RTW_API int rtw_device_count(int* count) {
@@ -1540,6 +1543,11 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->depth = std::max(1, depth);
     (void)hipDeviceGetAttribute(&g->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (g->cus <= 0) g->cus = 256;
+    {
+        int lm = 0;
+        if (hipDeviceGetAttribute(&lm, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lm > 0)
+            g->lds_max = lm;
+    }
     e = hipMalloc(&g->queue, 256);
     if (e != hipSuccess) {
         (void)hipFree(g->arena);
@@ -1610,8 +1618,8 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
 // fits, size the grid to the resident block count.
 int launch_render(rtw_gpu_world* g, KArgs& A, bool stats, hipStream_t stream) {
     const size_t scene_bytes = (size_t)(2 * g->node_count + g->leaf_count + (g->node_count + 1) / 2) * sizeof(float4);
-    const bool lds_scene = scene_bytes <= RTW_LDS_SCENE_MAX;
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
+    const bool lds_scene = scene_bytes <= RTW_LDS_SCENE_MAX && scene_bytes + stack_bytes <= (size_t)g->lds_max;
     const size_t lds = (lds_scene ? scene_bytes : 0) + stack_bytes;
     const void* fn;
     if (stats) fn = lds_scene ? (const void*)render_kernel<true, true> : (const void*)render_kernel<true, false>;

@@ -69,7 +69,7 @@ static int cull_pass(const float lo[3], const float hi[3], float k, float m, V o
     float D = 0.0f, t0[3], t1[3];
     for (int i = 0; i < 3; ++i) {
         const float a = lo[i] - o.e[i], b = hi[i] - o.e[i];
-        D += fmaxf(fabsf(a), fabsf(b));
+        D += fabsf(a) + fabsf(b);
         const float qa = a / d.e[i], qb = b / d.e[i];
         t0[i] = (qa < qb) ? qa : qb;
         t1[i] = (qa < qb) ? qb : qa;
@@ -91,7 +91,7 @@ static double outside(const float lo[3], const float hi[3], V o, V d, float t) {
 }
 static double delta_of(const float lo[3], const float hi[3], float k, float m, V o) {
     double D = 0.0;
-    for (int i = 0; i < 3; ++i) D += fmax(fabs((double)lo[i] - o.e[i]), fabs((double)hi[i] - o.e[i]));
+    for (int i = 0; i < 3; ++i) D += fabs((double)lo[i] - o.e[i]) + fabs((double)hi[i] - o.e[i]);
     return (double)k * D * D + 64.0 * 0x1p-24 * D + (double)m;
 }
 

@@ -30,7 +30,9 @@ def main():
               f"leaf {c['leaf_lanes']/it:.1f}, iters running node path {c['node_iters']/it:.2f} leaf path "
               f"{c['leaf_iters']/it:.2f}, lanes/shade {c['shade_lanes']/max(1,c['shade_calls']):.1f}, "
               f"shade calls/iter {c['shade_calls']/it:.3f}, alive lanes/iter {c['alive_lanes']/it:.1f}, "
-              f"waiting lanes/iter {c['wait_lanes']/it:.1f}", flush=True)
+              f"waiting lanes/iter {c['wait_lanes']/it:.1f}, passing lanes/iter {c['pass_lanes']/it:.1f}, "
+              f"inline near sphere: iters {c['sn_iters']/it:.2f} lanes/exec {c['sn_lanes']/max(1,c['sn_iters']):.1f}, "
+              f"far: iters {c['sf_iters']/it:.2f} lanes/exec {c['sf_lanes']/max(1,c['sf_iters']):.1f}", flush=True)
 
 
 if __name__ == "__main__":
