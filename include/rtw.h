@@ -260,8 +260,9 @@ RTW_API int rtw_render_collect_stats(rtw_gpu_world* gw, const rtw_render_params*
  * iterations that ran the node step, iterations that ran the leaf step, lane node steps, lane
  * leaf steps, live lanes and lanes waiting for shading (summed over iterations), lanes whose
  * node passed, iterations / lanes testing an inline near sphere child, the same for the far
- * child, shade calls, lanes shaded. */
-#define RTW_DEBUG_COUNTERS 15
+ * child, shade calls, lanes shaded, wave cycles in traversal, wave cycles elsewhere (refill,
+ * ray setup, shading). */
+#define RTW_DEBUG_COUNTERS 17
 RTW_API int rtw_render_debug_counters(rtw_gpu_world* gw, const rtw_render_params* params,
                                       rtw_render_stats* stats, uint64_t* counters, int n);
 /* Output encoder (color.rs:43-48 to_rgb8_gamma2), on the device: d_rgb8 gets W*H*3 bytes. */

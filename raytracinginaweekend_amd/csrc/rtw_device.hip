@@ -93,7 +93,8 @@ struct KArgs {
     uint32_t s_begin, s_end, chunk;
     uint64_t items;
     float* colors;
-    int32_t trace_min;       // dynamic ray fetch threshold (lanes still tracing)
+    int32_t trace_min;       // dynamic ray fetch threshold (lanes still tracing), exit mode 0
+    int32_t shade_ratio;     // exit mode 1: leave when waited lane-iterations * 10 >= tracing * shade_ratio
     const DWorld* wdev;      // a copy of `w` in device memory (for the out-of-line shader)
     uint64_t seed_key;
     float sx, sy;            // 1/(W-1), 1/(H-1)
@@ -166,7 +167,7 @@ enum {
 // resp. leaf path / lanes stepping a node resp. a leaf / shade calls / lanes shading
 enum { DB_TRAV_CALLS, DB_ITERS, DB_NODE_ITERS, DB_LEAF_ITERS, DB_NODE_LANES, DB_LEAF_LANES, DB_ALIVE_LANES,
        DB_WAIT_LANES, DB_PASS_LANES, DB_SN_ITERS, DB_SN_LANES, DB_SF_ITERS, DB_SF_LANES, DB_SHADE_CALLS,
-       DB_SHADE_LANES, DB_COUNT };
+       DB_SHADE_LANES, DB_TRAV_CYCLES, DB_REST_CYCLES, DB_COUNT };
 struct Stats {
     uint32_t c[ST_COUNT];
 };
@@ -878,7 +879,8 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 }
 
 template <bool STATS, bool LDS_SCENE>
-__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
+__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t shade_ratio,
+                                         int32_t n_nodes,
                                       int32_t n_leaves, unsigned long long* dbg) {
     const DWorld& w = *wp;
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
@@ -896,6 +898,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // first active lane of the wave (or of the branch) only
     uint32_t db[DB_SHADE_CALLS] = {};
     const bool lead0 = (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
+    uint32_t waited = 0;
     if (STATS && lead0) db[DB_TRAV_CALLS] = 1;
     // Each iteration a lane first tests the leaf it stands on, if any (popping the next item),
     // then tests the node it stands on, if any (pushing the far child, moving to the near one):
@@ -904,7 +907,17 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     for (;;) {
         const unsigned long long tr = __ballot(T.phase == PH_TRACE);
         if (tr == 0) break;
-        if (__popcll(tr) < (unsigned)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
+        {
+            const uint32_t nw = (uint32_t)__popcll(__ballot(T.phase == PH_SHADE));
+            if (shade_ratio <= 0) {
+                if ((uint32_t)__popcll(tr) < (uint32_t)trace_min && nw != 0) break;
+            } else {
+                // rent or buy: leave once the lane-iterations spent waiting since the last shading
+                // round outweigh what a shading round costs the lanes still tracing
+                waited += nw;
+                if (nw != 0 && waited * 10u >= (uint32_t)__popcll(tr) * (uint32_t)shade_ratio) break;
+            }
+        }
         if (STATS) {
             const unsigned long long lm = __ballot(T.phase == PH_TRACE && T.node < 0);
             const uint32_t alive = (uint32_t)__popcll(__ballot(1));
@@ -1019,6 +1032,7 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
     T.te = F32_INF;
     T.found = -1;
     bool fresh = false;  // T.ray is new: the traversal state must be initialised
+    uint64_t c_mark = STATS ? clock64() : 0;  // execution-time split (counting variant only)
 
     // rendering.rs:174-176: jitter (x then y), then Camera::ray
     auto start_sample = [&]() {
@@ -1073,6 +1087,12 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
         if (out_of_work) break;
 
         // 2. a new ray starts at the root (Scene::hit with t_range 0.001..inf, rendering.rs:25)
+        uint64_t c_trav = 0;
+        if (STATS) {
+            c_trav = clock64();
+            if (lane == __ffsll((long long)__ballot(1)) - 1)
+                atomicAdd(&A.stats[ST_COUNT + DB_REST_CYCLES], (unsigned long long)(c_trav - c_mark));
+        }
         if (fresh) {
             fresh = false;
             const RayPre rp = ray_pre(T.ray);
@@ -1086,8 +1106,13 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
         }
 
         // 3. traversal (hittable.rs:429-473)
-        T = traverse<STATS, LDS_SCENE>(A.wdev, T, A.trace_min, A.node_count, A.leaf_count,
+        T = traverse<STATS, LDS_SCENE>(A.wdev, T, A.trace_min, A.shade_ratio, A.node_count, A.leaf_count,
                                        STATS ? A.stats + ST_COUNT : nullptr);
+        if (STATS) {
+            c_mark = clock64();
+            if (lane == __ffsll((long long)__ballot(1)) - 1)
+                atomicAdd(&A.stats[ST_COUNT + DB_TRAV_CYCLES], (unsigned long long)(c_mark - c_trav));
+        }
         if (STATS) {
             st.c[ST_NODES] += T.n_nodes;
             st.c[ST_T_SPHERE] += T.n_sph_rect & 0xFFFFu;
@@ -1337,6 +1362,7 @@ struct rtw_gpu_world {
     int32_t node_count = 0, leaf_count = 0, depth = 1;
     int cus = 0;
     int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
+    int tuned_trace_min = 0;  // dynamic-fetch threshold picked by the first large render (0: not yet)
 };
 
 extern "C" RTW_API int rtw_device_count(int* count) {
@@ -1606,6 +1632,8 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.wdev = g->wdev;
     A.trace_min = 32;
     if (const char* e = getenv("RTW_TRACE_MIN")) A.trace_min = atoi(e);
+    A.shade_ratio = 0;
+    if (const char* e = getenv("RTW_SHADE_RATIO")) A.shade_ratio = atoi(e);
     A.seed_key = rtw_seed_key(p->seed);
     A.sx = 1.0f / (float)(p->width - 1);
     A.sy = 1.0f / (float)(p->height - 1);
@@ -1677,6 +1705,42 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
     }
     A.colors = g->colors;
     A.chunk = chunk;
+    // The best dynamic-fetch threshold depends on the world (how traversal and shading costs
+    // compare, how much ray lengths vary): the first render of >= 2^25 samples times one chunk of
+    // every pixel at a few thresholds and keeps the fastest (a one-off, synchronous ~4 x 10 ms;
+    // the image does not depend on it).  RTW_TRACE_MIN overrides.
+    if (!stats && !std::getenv("RTW_TRACE_MIN")) {
+        if (g->tuned_trace_min == 0 && (uint64_t)A.total * A.spp >= (1ull << 25)) {
+            static const int cand[] = {12, 20, 32, 48};
+            hipEvent_t e0, e1;
+            HIP_TRY(hipEventCreate(&e0));
+            HIP_TRY(hipEventCreate(&e1));
+            KArgs C = A;
+            C.s_begin = 0;
+            C.s_end = std::min<uint32_t>(A.spp, chunk);
+            C.items = A.total;
+            float best = 0.0f;
+            int best_tm = 32;
+            for (int i = 0; i < 4; ++i) {
+                C.trace_min = cand[i];
+                HIP_TRY(hipEventRecord(e0, stream));
+                rc = launch_render(g, C, false, stream);
+                if (rc != RTW_OK) return rc;
+                HIP_TRY(hipEventRecord(e1, stream));
+                HIP_TRY(hipEventSynchronize(e1));
+                float ms = 0.0f;
+                HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+                if (i == 0 || ms < best) {
+                    best = ms;
+                    best_tm = cand[i];
+                }
+            }
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            g->tuned_trace_min = best_tm;
+        }
+        if (g->tuned_trace_min > 0) A.trace_min = g->tuned_trace_min;
+    }
     for (uint32_t s0 = 0; s0 < A.spp; s0 += (uint32_t)per_launch) {
         const uint32_t s1 = (uint32_t)std::min<uint64_t>(A.spp, s0 + per_launch);
         A.s_begin = s0;

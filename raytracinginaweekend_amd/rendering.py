@@ -111,7 +111,7 @@ class DeviceWorld:
 
     DEBUG_COUNTERS = ("trav_calls", "iters", "node_iters", "leaf_iters", "node_lanes", "leaf_lanes",
                       "alive_lanes", "wait_lanes", "pass_lanes", "sn_iters", "sn_lanes", "sf_iters", "sf_lanes",
-                      "shade_calls", "shade_lanes")
+                      "shade_calls", "shade_lanes", "trav_cycles", "rest_cycles")
 
     def debug_counters(self, params: N.RenderParams) -> tuple[dict, dict]:
         """(statistics, wave-level execution counters) of one counting-variant render."""

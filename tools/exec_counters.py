@@ -32,7 +32,8 @@ def main():
               f"shade calls/iter {c['shade_calls']/it:.3f}, alive lanes/iter {c['alive_lanes']/it:.1f}, "
               f"waiting lanes/iter {c['wait_lanes']/it:.1f}, passing lanes/iter {c['pass_lanes']/it:.1f}, "
               f"inline near sphere: iters {c['sn_iters']/it:.2f} lanes/exec {c['sn_lanes']/max(1,c['sn_iters']):.1f}, "
-              f"far: iters {c['sf_iters']/it:.2f} lanes/exec {c['sf_lanes']/max(1,c['sf_iters']):.1f}", flush=True)
+              f"cycles/iter {c['trav_cycles']/it:.0f}, cycles/shade round {c['rest_cycles']/max(1,c['shade_calls']):.0f}, "
+              f"traversal share {c['trav_cycles']/max(1,c['trav_cycles']+c['rest_cycles']):.2f}", flush=True)
 
 
 if __name__ == "__main__":
