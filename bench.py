@@ -46,6 +46,43 @@ def alg_bytes(stats: dict, pixels: int) -> int:
     )
 
 
+def pmc_traffic(args) -> dict | None:
+    """HBM bytes of one render-kernel launch from rocprofv3 PMC counters (MI355X_MICROARCH.md
+    HBM section): a child `rocprofv3 --pmc FETCH_SIZE` run and a separate `--pmc WRITE_SIZE` run
+    of this same benchmark (1 frame, no warmup), each reading the frame's render_kernel dispatch.
+    FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 reports half the bytes of wide coalesced reads in
+    FETCH_SIZE, so it is doubled.  None if rocprofv3 is unavailable or a pass fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    if not shutil.which("rocprofv3"):
+        return None
+    child = [sys.executable, os.path.abspath(__file__), "--scene", args.scene, "--width", str(args.width), "--height",
+             str(args.height), "--spp", str(args.spp), "--max-depth", str(args.max_depth), "--seed", str(args.seed),
+             "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-stats", "--no-traffic"]
+    got = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+            cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "pmc", "--output-format", "csv", "--"] + child
+            try:
+                subprocess.run(cmd, check=True, capture_output=True, timeout=600, cwd=ROOT)
+            except (subprocess.SubprocessError, OSError):
+                return None
+            rows = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                rows += [r for r in csv.DictReader(open(f)) if "render_kernel" in r["Kernel_Name"]
+                         and r["Counter_Name"] == counter]
+            if not rows:
+                return None
+            last = max(rows, key=lambda r: int(r["Dispatch_Id"]))  # the frame (after autotune launches)
+            got[counter] = float(last["Counter_Value"]) * 1024.0
+    fetch = got["FETCH_SIZE"] * 2.0
+    return {"fetch_bytes": fetch, "write_bytes": got["WRITE_SIZE"], "bytes": fetch + got["WRITE_SIZE"]}
+
+
 def cpu_baseline(world, args) -> dict:
     """The reference algorithm on the host cores (oracle/, test infrastructure), on a bounded
     sample of the same frame: every P-th 8x8 tile (interleaved, like the GPU partition) at the
@@ -98,6 +135,7 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--save", default="", help="write the rank-0 image (.ppm/.png)")
@@ -165,7 +203,7 @@ def main() -> None:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "render_kernel<false>",
+            "kernel": "render_kernel<false, true> (HIP events also span the in-order accumulate_kernel)",
             "kernel_ms": round(kernel_ms, 3),
             "alg_bytes_per_launch": b,
             "per_sample": {k: round(v / max(1, stats["samples"]), 3) for k, v in stats.items() if k != "samples"},
@@ -174,6 +212,12 @@ def main() -> None:
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(world, args)
+    if roofline is not None and rank == 0 and world_size == 1 and not args.no_traffic:
+        t = pmc_traffic(args)
+        if t is not None:
+            roofline["traffic"] = round(t["bytes"])
+            roofline["traffic_detail"] = {"fetch_bytes_x2": round(t["fetch_bytes"]), "write_bytes": round(t["write_bytes"]),
+                                          "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one frame's render_kernel"}
 
     if args.save and rank == 0:
         import numpy as np

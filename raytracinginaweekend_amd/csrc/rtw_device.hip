@@ -993,7 +993,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 }
 
 template <bool STATS, bool LDS_SCENE>
-__global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
+__device__ __forceinline__ void render_body(const KArgs& A) {
     // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
     // per node)] [stack: depth x BLOCK]
     const DWorld& w = A.w;
@@ -1166,6 +1166,17 @@ __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kern
         for (int i = 0; i < ST_COUNT; ++i)
             if (st.c[i]) atomicAdd(&A.stats[i], (unsigned long long)st.c[i]);
     }
+}
+
+template <bool STATS, bool LDS_SCENE>
+__global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
+    render_body<STATS, LDS_SCENE>(A);
+}
+// the same code under another symbol, for the threshold calibration launches (so that profiles
+// of render_kernel contain frames only)
+template <bool LDS_SCENE>
+__global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void tune_kernel(KArgs A) {
+    render_body<false, LDS_SCENE>(A);
 }
 
 // Per slot: sum += colour of each sample of this launch, in sample order (the running sum of
@@ -1644,13 +1655,16 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
 
 // Launch the persistent render kernel: zero the pixel queue, stage the scene in LDS when it
 // fits, size the grid to the resident block count.
-int launch_render(rtw_gpu_world* g, KArgs& A, bool stats, hipStream_t stream) {
+enum LaunchKind { LK_RENDER, LK_STATS, LK_TUNE };
+int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
+    const bool stats = kind == LK_STATS;
     const size_t scene_bytes = (size_t)(2 * g->node_count + g->leaf_count + (g->node_count + 1) / 2) * sizeof(float4);
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
     const bool lds_scene = scene_bytes <= RTW_LDS_SCENE_MAX && scene_bytes + stack_bytes <= (size_t)g->lds_max;
     const size_t lds = (lds_scene ? scene_bytes : 0) + stack_bytes;
     const void* fn;
     if (stats) fn = lds_scene ? (const void*)render_kernel<true, true> : (const void*)render_kernel<true, false>;
+    else if (kind == LK_TUNE) fn = lds_scene ? (const void*)tune_kernel<true> : (const void*)tune_kernel<false>;
     else fn = lds_scene ? (const void*)render_kernel<false, true> : (const void*)render_kernel<false, false>;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;
@@ -1662,6 +1676,9 @@ int launch_render(rtw_gpu_world* g, KArgs& A, bool stats, hipStream_t stream) {
     if (stats) {
         if (lds_scene) hipLaunchKernelGGL((render_kernel<true, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
         else hipLaunchKernelGGL((render_kernel<true, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
+    } else if (kind == LK_TUNE) {
+        if (lds_scene) hipLaunchKernelGGL((tune_kernel<true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
+        else hipLaunchKernelGGL((tune_kernel<false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
     } else {
         if (lds_scene) hipLaunchKernelGGL((render_kernel<false, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
         else hipLaunchKernelGGL((render_kernel<false, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
@@ -1724,7 +1741,7 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
             for (int i = 0; i < 4; ++i) {
                 C.trace_min = cand[i];
                 HIP_TRY(hipEventRecord(e0, stream));
-                rc = launch_render(g, C, false, stream);
+                rc = launch_render(g, C, LK_TUNE, stream);
                 if (rc != RTW_OK) return rc;
                 HIP_TRY(hipEventRecord(e1, stream));
                 HIP_TRY(hipEventSynchronize(e1));
@@ -1746,7 +1763,7 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
         A.s_begin = s0;
         A.s_end = s1;
         A.items = (uint64_t)A.total * ((s1 - s0 + chunk - 1) / chunk);
-        rc = launch_render(g, A, stats, stream);
+        rc = launch_render(g, A, stats ? LK_STATS : LK_RENDER, stream);
         if (rc != RTW_OK) return rc;
         const unsigned blocks = (A.total + 255) / 256;
         hipLaunchKernelGGL(accumulate_kernel, dim3(blocks), dim3(256), 0, stream, (const float*)g->colors, s1 - s0,
