@@ -239,6 +239,15 @@ RTW_API int rtw_device_count(int* count);
 RTW_API int rtw_render(const rtw_world* world, const rtw_render_params* params, int device,
                        float* out_rgb);
 
+/* rtw_render with progress reports, the analogue of the reference's progress thread
+ * (rendering.rs:140-157): cb(done_samples, total_samples, user) is called from the calling
+ * thread about every 50 ms while the frame renders (done_samples counts finished work items of
+ * RTW_CHUNK samples), and once more with done == total before returning.  cb == NULL behaves
+ * like rtw_render. */
+typedef void (*rtw_progress_fn)(uint64_t done_samples, uint64_t total_samples, void* user);
+RTW_API int rtw_render_progress(const rtw_world* world, const rtw_render_params* params, int device,
+                                float* out_rgb, rtw_progress_fn cb, void* user);
+
 /* Resident path: upload once, render many times into device memory. */
 RTW_API int rtw_world_upload(const rtw_world* world, int device, rtw_gpu_world** out);
 RTW_API int rtw_world_release(rtw_gpu_world* gw);

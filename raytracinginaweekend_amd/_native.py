@@ -219,6 +219,9 @@ class Assets(C.Structure):
     ]
 
 
+PROGRESS_FN = C.CFUNCTYPE(None, C.c_uint64, C.c_uint64, C.c_void_p)  # rtw_progress_fn
+
+
 class RtwError(RuntimeError):
     def __init__(self, code: int, message: str):
         super().__init__(f"rtw error {code}: {message}")
@@ -239,6 +242,8 @@ _SIGS = {
     "rtw_partition_floats": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int64)]),
     "rtw_untile_device": (C.c_int, [C.POINTER(RenderParams), _P, C.c_int64, _P, _P]),
     "rtw_render_collect_stats": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(RenderStats)]),
+    "rtw_render_progress": (C.c_int, [C.POINTER(World), C.POINTER(RenderParams), C.c_int, C.POINTER(C.c_float),
+                                      _P, _P]),
     "rtw_render_debug_counters": (
         C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(RenderStats), C.POINTER(C.c_uint64), C.c_int]),
     "rtw_encode_rgb8_device": (C.c_int, [_P, C.c_int64, _P, _P]),

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <string>
 #include <vector>
 
@@ -93,6 +94,7 @@ struct KArgs {
     uint32_t s_begin, s_end, chunk;
     uint64_t items;
     float* colors;
+    unsigned long long* done; // finished work items of the frame (progress), or null
     int32_t trace_min;       // dynamic ray fetch threshold (lanes still tracing), exit mode 0
     int32_t shade_ratio;     // exit mode 1: leave when waited lane-iterations * 10 >= tracing * shade_ratio
     const DWorld* wdev;      // a copy of `w` in device memory (for the out-of-line shader)
@@ -283,9 +285,8 @@ __host__ __device__ __forceinline__ TriFast tri_prepare(V3 p0, V3 p1, V3 p2) {
     return f;
 }
 // 4 float4 per triangle: {p0.xyz, n.x} {n.yz, vt1.xy} {vt1.z, den1, vt2.xy} {vt2.z, den2, 0, 0}
-__device__ __forceinline__ TriFast load_tri(const DWorld& w, int i) {
-    const float4 a = w.tri_fast[4 * i], b = w.tri_fast[4 * i + 1], c = w.tri_fast[4 * i + 2],
-                 d = w.tri_fast[4 * i + 3];
+__device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i) {
+    const float4 a = tf[4 * i], b = tf[4 * i + 1], c = tf[4 * i + 2], d = tf[4 * i + 3];
     TriFast f;
     f.p0 = v3(a.x, a.y, a.z);
     f.n = v3(a.w, b.x, b.y);
@@ -294,6 +295,14 @@ __device__ __forceinline__ TriFast load_tri(const DWorld& w, int i) {
     f.vt2 = v3(c.z, c.w, d.x);
     f.den2 = d.y;
     return f;
+}
+// a wave-uniform pointer in scalar registers
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 // the per-ray part; barycentrics are recomputed from (ray, t) by leaf_record
 __device__ __forceinline__ bool tri_test(const TriFast& T, const Ray& r, float ts, float te, float& t) {
@@ -319,7 +328,7 @@ __device__ __forceinline__ bool geom_t(const DWorld& w, int kind, int idx, const
         return rect_t(load_rect(w, idx), r, ts, te, t, pos);
     }
     if (kind == RTW_GEOM_BOX) return box_t(w, idx, r, ts, te, t);
-    return tri_test(load_tri(w, idx), r, ts, te, t);
+    return tri_test(load_tri(w.tri_fast, idx), r, ts, te, t);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -447,7 +456,7 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         setc(sn, plane, rtw_signum(comp(pos, plane) - center));
         from_ray(h, rr, pos, sn, 0.0f, 0.0f);
     } else {  // triangle_geometry.rs:22-39
-        const TriFast T = load_tri(w, idx);
+        const TriFast T = load_tri(w.tri_fast, idx);
         const V3 pos = at(rr, t);
         const V3 q = sub(pos, T.p0);
         const float w1 = dot(q, T.vt1) / T.den1;
@@ -883,6 +892,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                                          int32_t n_nodes,
                                       int32_t n_leaves, unsigned long long* dbg) {
     const DWorld& w = *wp;
+    // the plain-triangle records' base, loaded once per call into scalar registers (the world
+    // struct is read through a pointer; left in the loop it becomes a dependent global load)
+    const float4* tri_fast = uniform_ptr(w.tri_fast);
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
     const float4* nodes_a = LDS_SCENE ? smem : w.node_a;
     const float4* nodes_b = LDS_SCENE ? smem + n_nodes : w.node_b;
@@ -939,7 +951,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             } else if (__float_as_int(sph.x) == 1) {  // a plain triangle
                 if (STATS) st.c[ST_T_TRI]++;
                 float t;
-                if (tri_test(load_tri(w, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) {
+                if (tri_test(load_tri(tri_fast, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) {
                     T.te = t;
                     T.found = leaf;
                 }
@@ -1020,6 +1032,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     uint32_t pix = 0, slot = 0;
     float fx = 0.0f, fy = 0.0f;
     uint32_t sample = 0, sample_end = 0;
+    bool finished = false;  // this lane completed a work item since its last refill (progress)
     V3 pdir = v3(0.0f, 0.0f, 0.0f), att = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
     int32_t depth = 0;
     Trav T;
@@ -1050,6 +1063,11 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     for (;;) {
         // 1. lanes without a pixel take the next ones (one atomic per wave per round)
         bool out_of_work = false;
+        if (A.done) {  // progress: one atomic per wave and refill round
+            const unsigned long long fm = __ballot(T.phase == PH_PIXEL && finished);
+            if (fm != 0 && lane == __ffsll((long long)fm) - 1) atomicAdd(A.done, (unsigned long long)__popcll(fm));
+            finished = false;
+        }
         for (;;) {
             const unsigned long long m = __ballot(T.phase == PH_PIXEL);
             if (m == 0) break;
@@ -1155,8 +1173,12 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 o[2] = so.color.z;
                 if (STATS) st.c[ST_SAMPLES]++;
                 ++sample;
-                if (sample >= sample_end) T.phase = PH_PIXEL;
-                else start_sample();
+                if (sample >= sample_end) {
+                    T.phase = PH_PIXEL;
+                    finished = true;
+                } else {
+                    start_sample();
+                }
             } else {
                 fresh = true;  // the scattered ray continues the path
             }
@@ -1707,8 +1729,13 @@ int grow(void** buf, size_t* have, size_t need) {
 
 // One frame: launches of at most RTW_SAMPLE_BUFFER_BYTES (default 16 GiB) of per-sample colours,
 // each followed by the in-order accumulation; work items of RTW_CHUNK (default 8) samples.
-int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream) {
+int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream, bool progress = false) {
     if (A.total == 0) return RTW_OK;
+    A.done = nullptr;
+    if (progress) {  // the second word of the queue allocation counts finished work items
+        A.done = g->queue + 1;
+        HIP_TRY(hipMemsetAsync(A.done, 0, sizeof(unsigned long long), stream));
+    }
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 8));
     const size_t budget = env_size("RTW_SAMPLE_BUFFER_BYTES", (size_t)16 << 30);
     const size_t per_sample = (size_t)A.total * 3 * sizeof(float);
@@ -1733,6 +1760,7 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
             HIP_TRY(hipEventCreate(&e0));
             HIP_TRY(hipEventCreate(&e1));
             KArgs C = A;
+            C.done = nullptr;
             C.s_begin = 0;
             C.s_end = std::min<uint32_t>(A.spp, chunk);
             C.items = A.total;
@@ -1876,6 +1904,76 @@ extern "C" RTW_API int rtw_render(const rtw_world* w, const rtw_render_params* p
         }
     }
     (void)hipFree(d);
+    rtw_world_release(g);
+    if (rc != RTW_OK) return rc;
+    if (e != hipSuccess) return rtw::fail(RTW_ERR_HIP, std::string("render: ") + hipGetErrorString(e));
+    return RTW_OK;
+}
+
+// rtw_render with progress reports (the reference's progress thread, rendering.rs:140-157): the
+// frame runs on its own stream while this thread polls the finished-work counter (a copy on a
+// second stream) every ~50 ms and calls cb(done_samples, total_samples, user); the last call
+// reports done == total.
+extern "C" RTW_API int rtw_render_progress(const rtw_world* w, const rtw_render_params* p, int device,
+                                           float* out_rgb, rtw_progress_fn cb, void* user) {
+    if (!p || !out_rgb) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    if (!cb) return rtw_render(w, p, device, out_rgb);
+    rtw_gpu_world* g = nullptr;
+    int rc = rtw_world_upload(w, device, &g);
+    if (rc != RTW_OK) return rc;
+    rtw_render_params q = *p;
+    q.layout = RTW_LAYOUT_IMAGE;
+    const size_t bytes = (size_t)q.width * (size_t)q.height * 3 * sizeof(float);
+    float* d = nullptr;
+    unsigned long long* h = nullptr;
+    hipStream_t rs = nullptr, ps = nullptr;
+    hipEvent_t fin = nullptr;
+    hipError_t e = hipMalloc(&d, bytes);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&rs, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&fin, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMemcpy(d, out_rgb, bytes, hipMemcpyHostToDevice);
+    const uint64_t total = (uint64_t)q.width * (uint64_t)q.height * q.samples_per_pixel;
+    if (e == hipSuccess) {
+        KArgs A;
+        rc = make_args(g, &q, A);
+        if (rc == RTW_OK) {
+            A.out = d;
+            const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 8));
+            rc = render_frame(g, A, false, d, rs, true);
+            if (rc == RTW_OK) e = hipEventRecord(fin, rs);
+            uint64_t last = ~0ull;
+            while (rc == RTW_OK && e == hipSuccess) {
+                const hipError_t qe = hipEventQuery(fin);
+                if (qe == hipSuccess) break;
+                if (qe != hipErrorNotReady) {
+                    e = qe;
+                    break;
+                }
+                *h = 0;
+                e = hipMemcpyAsync(h, A.done, sizeof(unsigned long long), hipMemcpyDeviceToHost, ps);
+                if (e == hipSuccess) e = hipStreamSynchronize(ps);
+                const uint64_t done = std::min<uint64_t>(total, (uint64_t)*h * chunk);
+                if (e == hipSuccess && done != last && done < total) {
+                    cb(done, total, user);
+                    last = done;
+                }
+                struct timespec ts = {0, 50 * 1000 * 1000};
+                nanosleep(&ts, nullptr);
+            }
+            if (rc == RTW_OK && e == hipSuccess) e = hipStreamSynchronize(rs);
+            if (rc == RTW_OK && e == hipSuccess) {
+                cb(total, total, user);
+                e = hipMemcpy(out_rgb, d, bytes, hipMemcpyDeviceToHost);
+            }
+        }
+    }
+    if (fin) (void)hipEventDestroy(fin);
+    if (ps) (void)hipStreamDestroy(ps);
+    if (rs) (void)hipStreamDestroy(rs);
+    if (h) (void)hipHostFree(h);
+    if (d) (void)hipFree(d);
     rtw_world_release(g);
     if (rc != RTW_OK) return rc;
     if (e != hipSuccess) return rtw::fail(RTW_ERR_HIP, std::string("render: ") + hipGetErrorString(e));

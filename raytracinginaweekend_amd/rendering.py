@@ -70,12 +70,22 @@ def render(
     *,
     seed: int = DEFAULT_SEED,
     device: int = 0,
+    progress=None,
 ) -> np.ndarray:
-    """Linear radiance, shape (H*W, 3) f32, row-major from the top-left pixel (Vec<Color>)."""
+    """Linear radiance, shape (H*W, 3) f32, row-major from the top-left pixel (Vec<Color>).
+
+    progress: optional callable(done_samples, total_samples), called about every 50 ms while the
+    frame renders and once at the end -- the reference's progress thread (rendering.rs:140-157)
+    reports the same quantity as a percentage on stderr."""
     del thread_count
     p = render_params(image_size, samples_per_pixel, max_depth, render_mode, seed)
     out = np.zeros((image_size.height * image_size.width, 3), np.float32)
-    check(lib().rtw_render(world.ptr(), C.byref(p), device, out.ctypes.data_as(C.POINTER(C.c_float))))
+    ptr = out.ctypes.data_as(C.POINTER(C.c_float))
+    if progress is None:
+        check(lib().rtw_render(world.ptr(), C.byref(p), device, ptr))
+    else:
+        cb = N.PROGRESS_FN(lambda done, total, _user: progress(int(done), int(total)))
+        check(lib().rtw_render_progress(world.ptr(), C.byref(p), device, ptr, C.cast(cb, C.c_void_p), None))
     return out
 
 

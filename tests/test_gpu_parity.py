@@ -105,3 +105,17 @@ def test_tile_partitions_reassemble_bit_exact(worlds, world_size):
     assert_bit_identical(image.cpu().numpy().reshape(-1, 3), full, "untile_device")
     host = untile_host(gathered.cpu().numpy(), spec.size, spec.tile, world_size, xs[0].stride)
     assert_bit_identical(host, full, "untile_host")
+
+
+def test_progress_callback_reports_and_keeps_bits(worlds):
+    """rtw_render_progress (the reference's progress thread, rendering.rs:140-157): monotone
+    (done, total) reports ending at total, and the image equals rtw_render's."""
+    world = worlds("final_scene1")
+    size = R.Size2i(1920, 1080)
+    seen = []
+    img = R.render(size, 1, 48, 50, world, seed=5, progress=lambda d, t: seen.append((d, t)))
+    total = 1920 * 1080 * 48
+    assert seen and seen[-1] == (total, total)
+    assert all(t == total for _, t in seen)
+    assert all(a[0] <= b[0] for a, b in zip(seen, seen[1:]))
+    assert_bit_identical(img, R.render(size, 1, 48, 50, world, seed=5), "progress render")
