@@ -248,6 +248,7 @@ def main() -> None:
                 "spp": args.spp,
                 "max_depth": args.max_depth,
                 "partition": f"interleaved {spec.tile[0]}x{spec.tile[1]} tiles over {world_size} GPU(s)",
+                "trace_min": fr.dworld.tuned_trace_min(),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -251,6 +251,10 @@ RTW_API int rtw_render_progress(const rtw_world* world, const rtw_render_params*
 /* Resident path: upload once, render many times into device memory. */
 RTW_API int rtw_world_upload(const rtw_world* world, int device, rtw_gpu_world** out);
 RTW_API int rtw_world_release(rtw_gpu_world* gw);
+/* The dynamic ray-fetch threshold this world's renders settled on (tuned on the device during
+ * the first long render; 0 while still exploring).  Synchronous; performance only -- images do
+ * not depend on it. */
+RTW_API int rtw_world_tuning(rtw_gpu_world* gw, int* trace_min);
 /* Renders this partition's tiles into device buffer `d_out` (layout per params->layout) on
  * `stream` (a hipStream_t, NULL = default stream).  Asynchronous: returns after the launch. */
 RTW_API int rtw_render_device(rtw_gpu_world* gw, const rtw_render_params* params, float* d_out,

@@ -238,6 +238,7 @@ _SIGS = {
     "rtw_render": (C.c_int, [C.POINTER(World), C.POINTER(RenderParams), C.c_int, C.POINTER(C.c_float)]),
     "rtw_world_upload": (C.c_int, [C.POINTER(World), C.c_int, C.POINTER(_P)]),
     "rtw_world_release": (C.c_int, [_P]),
+    "rtw_world_tuning": (C.c_int, [_P, C.POINTER(C.c_int)]),
     "rtw_render_device": (C.c_int, [_P, C.POINTER(RenderParams), _P, _P]),
     "rtw_partition_floats": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int64)]),
     "rtw_untile_device": (C.c_int, [C.POINTER(RenderParams), _P, C.c_int64, _P, _P]),
@@ -299,6 +300,8 @@ def lib() -> C.CDLL:
             )
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("RTW_LIBRARY") and not hasattr(L, name):
+                continue  # an older experiment build (A/B runs only); the product library has them all
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
@@ -76,6 +77,20 @@ struct WorldConst {
     rtw_background bg;
 };
 
+// On-device tuning of the dynamic-fetch threshold, kept per world.  A launch that finds chosen == 0
+// runs exploration epochs of RTW_TUNE_EPOCH_TICKS (100 MHz clock): candidate cand[e] (mirrored,
+// a..f f..a) in epoch e, recording the work-item counter at each epoch start; after the last
+// epoch every wave derives the same winner (most items handed out per candidate) and publishes it.
+#define RTW_TUNE_NCAND 6
+#define RTW_TUNE_EPOCHS (2 * RTW_TUNE_NCAND)
+#define RTW_TUNE_EPOCH_TICKS 400000ull  // 4 ms
+struct TuneState {
+    unsigned long long t0;                          // clock at the first refill (~0: unset)
+    unsigned long long start[RTW_TUNE_EPOCHS + 1];  // work-item counter at each epoch start
+    int chosen;                                     // the world's threshold once decided (0: not yet)
+};
+__constant__ const int kTuneCand[RTW_TUNE_NCAND] = {12, 16, 24, 32, 40, 48};
+
 struct KArgs {
     DWorld w;
     int32_t width, height;
@@ -92,17 +107,23 @@ struct KArgs {
     // consecutive samples (item = chunk index * total + slot); each finished sample's colour goes
     // to colors[(sample - s_begin) * total + slot] and accumulate_kernel sums them in order
     uint32_t s_begin, s_end, chunk;
+    // samples [s_split, s_end) are handed out one per item (after the chunked ones): a launch then
+    // drains on single samples, not on whole chunks of the rare very long paths (paths trapped
+    // inside a mesh take ~100x the mean)
+    uint32_t s_split;
+    uint64_t items_big;  // items of the chunked range
     uint64_t items;
     float* colors;
-    unsigned long long* done; // finished work items of the frame (progress), or null
     int32_t trace_min;       // dynamic ray fetch threshold (lanes still tracing), exit mode 0
-    int32_t shade_ratio;     // exit mode 1: leave when waited lane-iterations * 10 >= tracing * shade_ratio
+    int32_t trace_hi;        // ... or below trace_hi once lanes have waited wait_cap iterations
+    int32_t wait_cap;
     const DWorld* wdev;      // a copy of `w` in device memory (for the out-of-line shader)
     uint64_t seed_key;
     float sx, sy;            // 1/(W-1), 1/(H-1)
     rtw_uniform ux, uy;      // pixel jitter distributions
     float* out;
     unsigned long long* stats; // 13 counters (stats variant only)
+    TuneState* tune;          // in-frame threshold tuning, or null
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -888,8 +909,8 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 }
 
 template <bool STATS, bool LDS_SCENE>
-__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t shade_ratio,
-                                         int32_t n_nodes,
+__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t trace_hi,
+                                         int32_t wait_cap, int32_t n_nodes,
                                       int32_t n_leaves, unsigned long long* dbg) {
     const DWorld& w = *wp;
     // the plain-triangle records' base, loaded once per call into scalar registers (the world
@@ -921,13 +942,15 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         if (tr == 0) break;
         {
             const uint32_t nw = (uint32_t)__popcll(__ballot(T.phase == PH_SHADE));
-            if (shade_ratio <= 0) {
-                if ((uint32_t)__popcll(tr) < (uint32_t)trace_min && nw != 0) break;
-            } else {
-                // rent or buy: leave once the lane-iterations spent waiting since the last shading
-                // round outweigh what a shading round costs the lanes still tracing
-                waited += nw;
-                if (nw != 0 && waited * 10u >= (uint32_t)__popcll(tr) * (uint32_t)shade_ratio) break;
+            // Leave for shading when fewer than trace_min lanes still trace, or -- once lanes have
+            // waited wait_cap iterations -- fewer than trace_hi: with uniform ray lengths the
+            // stragglers finish soon and deep batches pay; heavy-tailed ones (paths trapped in a
+            // mesh) would otherwise hold most lanes idle.
+            if (nw != 0) {
+                ++waited;
+                const uint32_t nt = (uint32_t)__popcll(tr);
+                if (nt < (uint32_t)trace_min || (wait_cap > 0 && waited >= (uint32_t)wait_cap && nt < (uint32_t)trace_hi))
+                    break;
             }
         }
         if (STATS) {
@@ -1032,7 +1055,6 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     uint32_t pix = 0, slot = 0;
     float fx = 0.0f, fy = 0.0f;
     uint32_t sample = 0, sample_end = 0;
-    bool finished = false;  // this lane completed a work item since its last refill (progress)
     V3 pdir = v3(0.0f, 0.0f, 0.0f), att = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
     int32_t depth = 0;
     Trav T;
@@ -1060,14 +1082,58 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         fresh = true;
     };
 
+    int32_t trace_min = A.trace_min;  // this wave's dynamic-fetch threshold (tuned below)
+    bool tuned = A.tune == nullptr;
     for (;;) {
+        if (!tuned) {  // wave-uniform: scalar loads and a leader's atomics
+            const int ch = __hip_atomic_load(&A.tune->chosen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ch > 0) {
+                trace_min = ch;
+                tuned = true;
+            } else {
+                const bool leader = lane == __ffsll((long long)__ballot(1)) - 1;
+                const unsigned long long now = wall_clock64();
+                unsigned long long t0 = __hip_atomic_load(&A.tune->t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (t0 == ~0ull) {
+                    if (leader) atomicCAS(&A.tune->t0, ~0ull, now);
+                    t0 = now;
+                }
+                const unsigned long long e = (now - t0) / RTW_TUNE_EPOCH_TICKS;
+                if (e <= (unsigned long long)RTW_TUNE_EPOCHS) {
+                    if (leader &&
+                        __hip_atomic_load(&A.tune->start[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ~0ull)
+                        atomicCAS(&A.tune->start[e], ~0ull,
+                                  __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    trace_min = e < RTW_TUNE_EPOCHS
+                                    ? kTuneCand[e < RTW_TUNE_NCAND ? e : RTW_TUNE_EPOCHS - 1 - e]
+                                    : A.trace_min;
+                } else {
+                    unsigned long long st[RTW_TUNE_EPOCHS + 1];
+                    bool ok = true;
+                    for (int i = 0; i <= RTW_TUNE_EPOCHS; ++i) {
+                        st[i] = __hip_atomic_load(&A.tune->start[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = ok && st[i] != ~0ull && (i == 0 || st[i] >= st[i - 1]);
+                    }
+                    int best = A.trace_min;
+                    if (ok) {
+                        unsigned long long best_n = 0;
+                        for (int c = 0; c < RTW_TUNE_NCAND; ++c) {
+                            const unsigned long long n =
+                                (st[c + 1] - st[c]) + (st[RTW_TUNE_EPOCHS - c] - st[RTW_TUNE_EPOCHS - 1 - c]);
+                            if (c == 0 || n > best_n) {
+                                best_n = n;
+                                best = kTuneCand[c];
+                            }
+                        }
+                        if (leader) atomicCAS(&A.tune->chosen, 0, best);
+                    }
+                    trace_min = best;
+                    tuned = ok;
+                }
+            }
+        }
         // 1. lanes without a pixel take the next ones (one atomic per wave per round)
         bool out_of_work = false;
-        if (A.done) {  // progress: one atomic per wave and refill round
-            const unsigned long long fm = __ballot(T.phase == PH_PIXEL && finished);
-            if (fm != 0 && lane == __ffsll((long long)fm) - 1) atomicAdd(A.done, (unsigned long long)__popcll(fm));
-            finished = false;
-        }
         for (;;) {
             const unsigned long long m = __ballot(T.phase == PH_PIXEL);
             if (m == 0) break;
@@ -1082,8 +1148,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     out_of_work = true;
                     T.phase = PH_TRACE;  // leaves the loops below
                 } else {
-                    const uint32_t ck = (uint32_t)(item / A.total);
-                    const uint32_t c = (uint32_t)(item - (uint64_t)ck * A.total);
+                    const bool big = item < A.items_big;
+                    const uint64_t rel = big ? item : item - A.items_big;
+                    const uint32_t ck = (uint32_t)(rel / A.total);
+                    const uint32_t c = (uint32_t)(rel - (uint64_t)ck * A.total);
                     const int32_t lt = (int32_t)(c / (uint32_t)per_tile);
                     const int32_t it = (int32_t)(c % (uint32_t)per_tile);
                     const int32_t tile = A.part_index + lt * A.part_count;
@@ -1094,8 +1162,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         pix = (uint32_t)(py * A.width + px);
                         fx = (float)px * A.sx;  // size2i.rs:52-55
                         fy = (float)py * A.sy;
-                        sample = A.s_begin + ck * A.chunk;
-                        sample_end = min(sample + A.chunk, A.s_end);
+                        sample = big ? A.s_begin + ck * A.chunk : A.s_split + ck;
+                        sample_end = big ? min(sample + A.chunk, A.s_split) : sample + 1;
                         start_sample();
                         T.phase = PH_TRACE;
                     }
@@ -1124,7 +1192,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
 
         // 3. traversal (hittable.rs:429-473)
-        T = traverse<STATS, LDS_SCENE>(A.wdev, T, A.trace_min, A.shade_ratio, A.node_count, A.leaf_count,
+        T = traverse<STATS, LDS_SCENE>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.trace_hi, A.wait_cap, A.node_count, A.leaf_count,
                                        STATS ? A.stats + ST_COUNT : nullptr);
         if (STATS) {
             c_mark = clock64();
@@ -1173,12 +1241,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 o[2] = so.color.z;
                 if (STATS) st.c[ST_SAMPLES]++;
                 ++sample;
-                if (sample >= sample_end) {
-                    T.phase = PH_PIXEL;
-                    finished = true;
-                } else {
-                    start_sample();
-                }
+                if (sample >= sample_end) T.phase = PH_PIXEL;
+                else start_sample();
             } else {
                 fresh = true;  // the scattered ray continues the path
             }
@@ -1194,13 +1258,6 @@ template <bool STATS, bool LDS_SCENE>
 __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
     render_body<STATS, LDS_SCENE>(A);
 }
-// the same code under another symbol, for the threshold calibration launches (so that profiles
-// of render_kernel contain frames only)
-template <bool LDS_SCENE>
-__global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void tune_kernel(KArgs A) {
-    render_body<false, LDS_SCENE>(A);
-}
-
 // Per slot: sum += colour of each sample of this launch, in sample order (the running sum of
 // earlier launches is carried in `running`); the last launch writes sum / spp (rendering.rs:179;
 // merge_planes with one plane multiplies by 1.0).
@@ -1395,7 +1452,7 @@ struct rtw_gpu_world {
     int32_t node_count = 0, leaf_count = 0, depth = 1;
     int cus = 0;
     int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
-    int tuned_trace_min = 0;  // dynamic-fetch threshold picked by the first large render (0: not yet)
+    TuneState* tune = nullptr;  // in-frame threshold tuning state
 };
 
 extern "C" RTW_API int rtw_device_count(int* count) {
@@ -1607,7 +1664,9 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         if (hipDeviceGetAttribute(&lm, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lm > 0)
             g->lds_max = lm;
     }
-    e = hipMalloc(&g->queue, 256);
+    e = hipMalloc(&g->tune, sizeof(TuneState));
+    if (e == hipSuccess) e = hipMemset(g->tune, 0, sizeof(TuneState));
+    if (e == hipSuccess) e = hipMalloc(&g->queue, 256);
     if (e != hipSuccess) {
         (void)hipFree(g->arena);
         delete g;
@@ -1617,12 +1676,22 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     return RTW_OK;
 }
 
+extern "C" RTW_API int rtw_world_tuning(rtw_gpu_world* g, int* trace_min) {
+    if (!g || !trace_min) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(g->device));
+    int v = 0;
+    HIP_TRY(hipMemcpy(&v, &g->tune->chosen, sizeof(int), hipMemcpyDeviceToHost));
+    *trace_min = v;
+    return RTW_OK;
+}
+
 extern "C" RTW_API int rtw_world_release(rtw_gpu_world* g) {
     if (!g) return RTW_OK;
     (void)hipSetDevice(g->device);
     if (g->arena) (void)hipFree(g->arena);
     if (g->queue) (void)hipFree(g->queue);
     if (g->colors) (void)hipFree(g->colors);
+    if (g->tune) (void)hipFree(g->tune);
     if (g->running) (void)hipFree(g->running);
     delete g;
     return RTW_OK;
@@ -1665,8 +1734,10 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.wdev = g->wdev;
     A.trace_min = 32;
     if (const char* e = getenv("RTW_TRACE_MIN")) A.trace_min = atoi(e);
-    A.shade_ratio = 0;
-    if (const char* e = getenv("RTW_SHADE_RATIO")) A.shade_ratio = atoi(e);
+    A.trace_hi = 48;
+    if (const char* e = getenv("RTW_TRACE_HI")) A.trace_hi = atoi(e);
+    A.wait_cap = 0;
+    if (const char* e = getenv("RTW_WAIT_CAP")) A.wait_cap = atoi(e);
     A.seed_key = rtw_seed_key(p->seed);
     A.sx = 1.0f / (float)(p->width - 1);
     A.sy = 1.0f / (float)(p->height - 1);
@@ -1677,7 +1748,7 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
 
 // Launch the persistent render kernel: zero the pixel queue, stage the scene in LDS when it
 // fits, size the grid to the resident block count.
-enum LaunchKind { LK_RENDER, LK_STATS, LK_TUNE };
+enum LaunchKind { LK_RENDER, LK_STATS };
 int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const bool stats = kind == LK_STATS;
     const size_t scene_bytes = (size_t)(2 * g->node_count + g->leaf_count + (g->node_count + 1) / 2) * sizeof(float4);
@@ -1686,7 +1757,6 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const size_t lds = (lds_scene ? scene_bytes : 0) + stack_bytes;
     const void* fn;
     if (stats) fn = lds_scene ? (const void*)render_kernel<true, true> : (const void*)render_kernel<true, false>;
-    else if (kind == LK_TUNE) fn = lds_scene ? (const void*)tune_kernel<true> : (const void*)tune_kernel<false>;
     else fn = lds_scene ? (const void*)render_kernel<false, true> : (const void*)render_kernel<false, false>;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;
@@ -1694,13 +1764,10 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     if (per_cu < 1) return rtw::fail(RTW_ERR_UNSUPPORTED, "render kernel does not fit on a CU");
     const int64_t want = (int64_t)((A.items + RTW_BLOCK - 1) / RTW_BLOCK);
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per_cu * g->cus));
-    HIP_TRY(hipMemsetAsync(g->queue, 0, sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(A.queue, 0, sizeof(unsigned long long), stream));
     if (stats) {
         if (lds_scene) hipLaunchKernelGGL((render_kernel<true, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
         else hipLaunchKernelGGL((render_kernel<true, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
-    } else if (kind == LK_TUNE) {
-        if (lds_scene) hipLaunchKernelGGL((tune_kernel<true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
-        else hipLaunchKernelGGL((tune_kernel<false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
     } else {
         if (lds_scene) hipLaunchKernelGGL((render_kernel<false, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
         else hipLaunchKernelGGL((render_kernel<false, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
@@ -1709,11 +1776,24 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     return RTW_OK;
 }
 
+// work items of one launch: chunks of `chunk` samples, then the last RTW_TAIL_SAMPLES (default 8)
+// samples of the launch's range one at a time
+void set_items(KArgs& A, uint32_t chunk);
+
 size_t env_size(const char* name, size_t dflt) {
     const char* e = std::getenv(name);
     if (!e || !e[0]) return dflt;
     const long long v = std::atoll(e);
     return v > 0 ? (size_t)v : dflt;
+}
+
+void set_items(KArgs& A, uint32_t chunk) {
+    const uint32_t n = A.s_end - A.s_begin;
+    const uint32_t tail = std::min<uint32_t>(n, (uint32_t)env_size("RTW_TAIL_SAMPLES", 8));
+    A.chunk = chunk;
+    A.s_split = A.s_end - tail;
+    A.items_big = (uint64_t)A.total * ((A.s_split - A.s_begin + chunk - 1) / chunk);
+    A.items = A.items_big + (uint64_t)A.total * tail;
 }
 
 int grow(void** buf, size_t* have, size_t need) {
@@ -1729,13 +1809,12 @@ int grow(void** buf, size_t* have, size_t need) {
 
 // One frame: launches of at most RTW_SAMPLE_BUFFER_BYTES (default 16 GiB) of per-sample colours,
 // each followed by the in-order accumulation; work items of RTW_CHUNK (default 8) samples.
-int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream, bool progress = false) {
+// Launch l of a frame takes its work items from counter min(l, RTW_QUEUE_SLOTS - 1) of the
+// world's queue block, so a progress poller can read how many items each launch has handed out.
+#define RTW_QUEUE_SLOTS 32
+int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream,
+                 std::vector<uint64_t>* launch_items = nullptr) {
     if (A.total == 0) return RTW_OK;
-    A.done = nullptr;
-    if (progress) {  // the second word of the queue allocation counts finished work items
-        A.done = g->queue + 1;
-        HIP_TRY(hipMemsetAsync(A.done, 0, sizeof(unsigned long long), stream));
-    }
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 8));
     const size_t budget = env_size("RTW_SAMPLE_BUFFER_BYTES", (size_t)16 << 30);
     const size_t per_sample = (size_t)A.total * 3 * sizeof(float);
@@ -1749,48 +1828,23 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
     }
     A.colors = g->colors;
     A.chunk = chunk;
-    // The best dynamic-fetch threshold depends on the world (how traversal and shading costs
-    // compare, how much ray lengths vary): the first render of >= 2^25 samples times one chunk of
-    // every pixel at a few thresholds and keeps the fastest (a one-off, synchronous ~4 x 10 ms;
-    // the image does not depend on it).  RTW_TRACE_MIN overrides.
+    // In-frame tuning of the dynamic-fetch threshold (TuneState): until a world has chosen one,
+    // each render launch explores candidates over timed epochs on the device.  RTW_TRACE_MIN
+    // fixes the threshold instead.
+    A.tune = nullptr;
     if (!stats && !std::getenv("RTW_TRACE_MIN")) {
-        if (g->tuned_trace_min == 0 && (uint64_t)A.total * A.spp >= (1ull << 25)) {
-            static const int cand[] = {12, 20, 32, 48};
-            hipEvent_t e0, e1;
-            HIP_TRY(hipEventCreate(&e0));
-            HIP_TRY(hipEventCreate(&e1));
-            KArgs C = A;
-            C.done = nullptr;
-            C.s_begin = 0;
-            C.s_end = std::min<uint32_t>(A.spp, chunk);
-            C.items = A.total;
-            float best = 0.0f;
-            int best_tm = 32;
-            for (int i = 0; i < 4; ++i) {
-                C.trace_min = cand[i];
-                HIP_TRY(hipEventRecord(e0, stream));
-                rc = launch_render(g, C, LK_TUNE, stream);
-                if (rc != RTW_OK) return rc;
-                HIP_TRY(hipEventRecord(e1, stream));
-                HIP_TRY(hipEventSynchronize(e1));
-                float ms = 0.0f;
-                HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-                if (i == 0 || ms < best) {
-                    best = ms;
-                    best_tm = cand[i];
-                }
-            }
-            (void)hipEventDestroy(e0);
-            (void)hipEventDestroy(e1);
-            g->tuned_trace_min = best_tm;
-        }
-        if (g->tuned_trace_min > 0) A.trace_min = g->tuned_trace_min;
+        A.tune = g->tune;
+        HIP_TRY(hipMemsetAsync(g->tune, 0xFF, offsetof(TuneState, chosen), stream));
     }
-    for (uint32_t s0 = 0; s0 < A.spp; s0 += (uint32_t)per_launch) {
+    HIP_TRY(hipMemsetAsync(g->queue, 0, RTW_QUEUE_SLOTS * sizeof(unsigned long long), stream));
+    int launch = 0;
+    for (uint32_t s0 = 0; s0 < A.spp; s0 += (uint32_t)per_launch, ++launch) {
         const uint32_t s1 = (uint32_t)std::min<uint64_t>(A.spp, s0 + per_launch);
         A.s_begin = s0;
         A.s_end = s1;
-        A.items = (uint64_t)A.total * ((s1 - s0 + chunk - 1) / chunk);
+        set_items(A, chunk);
+        A.queue = g->queue + std::min(launch, RTW_QUEUE_SLOTS - 1);
+        if (launch_items) launch_items->push_back(A.items);
         rc = launch_render(g, A, stats ? LK_STATS : LK_RENDER, stream);
         if (rc != RTW_OK) return rc;
         const unsigned blocks = (A.total + 255) / 256;
@@ -1911,9 +1965,9 @@ extern "C" RTW_API int rtw_render(const rtw_world* w, const rtw_render_params* p
 }
 
 // rtw_render with progress reports (the reference's progress thread, rendering.rs:140-157): the
-// frame runs on its own stream while this thread polls the finished-work counter (a copy on a
-// second stream) every ~50 ms and calls cb(done_samples, total_samples, user); the last call
-// reports done == total.
+// frame runs on its own stream while this thread polls the launches' work-item counters (a copy
+// on a second stream) every ~50 ms and calls cb(done_samples, total_samples, user), done being
+// the share of work items handed out; the last call reports done == total.
 extern "C" RTW_API int rtw_render_progress(const rtw_world* w, const rtw_render_params* p, int device,
                                            float* out_rgb, rtw_progress_fn cb, void* user) {
     if (!p || !out_rgb) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
@@ -1929,7 +1983,7 @@ extern "C" RTW_API int rtw_render_progress(const rtw_world* w, const rtw_render_
     hipStream_t rs = nullptr, ps = nullptr;
     hipEvent_t fin = nullptr;
     hipError_t e = hipMalloc(&d, bytes);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&h, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h, RTW_QUEUE_SLOTS * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&rs, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&fin, hipEventDisableTiming);
@@ -1940,8 +1994,10 @@ extern "C" RTW_API int rtw_render_progress(const rtw_world* w, const rtw_render_
         rc = make_args(g, &q, A);
         if (rc == RTW_OK) {
             A.out = d;
-            const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 8));
-            rc = render_frame(g, A, false, d, rs, true);
+            std::vector<uint64_t> items;
+            rc = render_frame(g, A, false, d, rs, &items);
+            uint64_t all = 0;
+            for (uint64_t n : items) all += n;
             if (rc == RTW_OK) e = hipEventRecord(fin, rs);
             uint64_t last = ~0ull;
             while (rc == RTW_OK && e == hipSuccess) {
@@ -1951,10 +2007,12 @@ extern "C" RTW_API int rtw_render_progress(const rtw_world* w, const rtw_render_
                     e = qe;
                     break;
                 }
-                *h = 0;
-                e = hipMemcpyAsync(h, A.done, sizeof(unsigned long long), hipMemcpyDeviceToHost, ps);
+                e = hipMemcpyAsync(h, g->queue, RTW_QUEUE_SLOTS * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                   ps);
                 if (e == hipSuccess) e = hipStreamSynchronize(ps);
-                const uint64_t done = std::min<uint64_t>(total, (uint64_t)*h * chunk);
+                uint64_t taken = 0;
+                for (size_t l = 0; l < items.size() && l < RTW_QUEUE_SLOTS; ++l) taken += std::min<uint64_t>(h[l], items[l]);
+                const uint64_t done = all ? (uint64_t)((double)total * (double)taken / (double)all) : 0;
                 if (e == hipSuccess && done != last && done < total) {
                     cb(done, total, user);
                     last = done;

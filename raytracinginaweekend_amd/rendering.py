@@ -114,6 +114,12 @@ class DeviceWorld:
         """Asynchronous launch on `stream_ptr` (hipStream_t) into device pointer `d_out_ptr`."""
         check(lib().rtw_render_device(self._h, C.byref(params), C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr or 0)))
 
+    def tuned_trace_min(self) -> int:
+        """The dynamic ray-fetch threshold the device settled on (0 while still exploring)."""
+        v = C.c_int()
+        check(lib().rtw_world_tuning(self._h, C.byref(v)))
+        return v.value
+
     def collect_stats(self, params: N.RenderParams) -> dict:
         s = N.RenderStats()
         check(lib().rtw_render_collect_stats(self._h, C.byref(params), C.byref(s)))
