@@ -5,6 +5,7 @@ The product is librtw.so (HIP megakernel for gfx950 + host scene builder, C ABI 
 include/rtw.h).  This package is its Python face, mirroring the reference's interface:
 Camera.build()..., WorldBuilder / NodeBuilder, demo worlds, rendering.render(...).
 """
+from . import image_io
 from .rendering import DeviceWorld, RenderMode, Size2i, device_count, render, render_params
 from .world import (
     DEMO_WORLDS,
