@@ -115,8 +115,6 @@ struct KArgs {
     uint64_t items;
     float* colors;
     int32_t trace_min;       // dynamic ray fetch threshold (lanes still tracing), exit mode 0
-    int32_t trace_hi;        // ... or below trace_hi once lanes have waited wait_cap iterations
-    int32_t wait_cap;
     const DWorld* wdev;      // a copy of `w` in device memory (for the out-of-line shader)
     uint64_t seed_key;
     float sx, sy;            // 1/(W-1), 1/(H-1)
@@ -909,8 +907,7 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 }
 
 template <bool STATS, bool LDS_SCENE>
-__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t trace_hi,
-                                         int32_t wait_cap, int32_t n_nodes,
+__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
                                       int32_t n_leaves, unsigned long long* dbg) {
     const DWorld& w = *wp;
     // the plain-triangle records' base, loaded once per call into scalar registers (the world
@@ -931,7 +928,6 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // first active lane of the wave (or of the branch) only
     uint32_t db[DB_SHADE_CALLS] = {};
     const bool lead0 = (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
-    uint32_t waited = 0;
     if (STATS && lead0) db[DB_TRAV_CALLS] = 1;
     // Each iteration a lane first tests the leaf it stands on, if any (popping the next item),
     // then tests the node it stands on, if any (pushing the far child, moving to the near one):
@@ -940,19 +936,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     for (;;) {
         const unsigned long long tr = __ballot(T.phase == PH_TRACE);
         if (tr == 0) break;
-        {
-            const uint32_t nw = (uint32_t)__popcll(__ballot(T.phase == PH_SHADE));
-            // Leave for shading when fewer than trace_min lanes still trace, or -- once lanes have
-            // waited wait_cap iterations -- fewer than trace_hi: with uniform ray lengths the
-            // stragglers finish soon and deep batches pay; heavy-tailed ones (paths trapped in a
-            // mesh) would otherwise hold most lanes idle.
-            if (nw != 0) {
-                ++waited;
-                const uint32_t nt = (uint32_t)__popcll(tr);
-                if (nt < (uint32_t)trace_min || (wait_cap > 0 && waited >= (uint32_t)wait_cap && nt < (uint32_t)trace_hi))
-                    break;
-            }
-        }
+        // dynamic ray fetch: leave for shading when fewer than trace_min lanes still trace and some
+        // lane waits (the threshold is tuned per world on the device, see TuneState)
+        if ((uint32_t)__popcll(tr) < (uint32_t)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
         if (STATS) {
             const unsigned long long lm = __ballot(T.phase == PH_TRACE && T.node < 0);
             const uint32_t alive = (uint32_t)__popcll(__ballot(1));
@@ -1192,7 +1178,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
 
         // 3. traversal (hittable.rs:429-473)
-        T = traverse<STATS, LDS_SCENE>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.trace_hi, A.wait_cap, A.node_count, A.leaf_count,
+        T = traverse<STATS, LDS_SCENE>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, A.leaf_count,
                                        STATS ? A.stats + ST_COUNT : nullptr);
         if (STATS) {
             c_mark = clock64();
@@ -1734,10 +1720,6 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.wdev = g->wdev;
     A.trace_min = 32;
     if (const char* e = getenv("RTW_TRACE_MIN")) A.trace_min = atoi(e);
-    A.trace_hi = 48;
-    if (const char* e = getenv("RTW_TRACE_HI")) A.trace_hi = atoi(e);
-    A.wait_cap = 0;
-    if (const char* e = getenv("RTW_WAIT_CAP")) A.wait_cap = atoi(e);
     A.seed_key = rtw_seed_key(p->seed);
     A.sx = 1.0f / (float)(p->width - 1);
     A.sy = 1.0f / (float)(p->height - 1);
