@@ -148,6 +148,11 @@ def untile_device(params: N.RenderParams, d_tiles: int, stride_floats: int, d_im
                                   C.c_void_p(stream_ptr or 0)))
 
 
+def encode_rgb8_device(d_image: int, pixels: int, d_rgb8: int, stream_ptr: int | None = None) -> None:
+    """to_rgb8_gamma2 (color.rs:43-48) on the device: W*H*3 f32 at d_image -> W*H*3 bytes at d_rgb8."""
+    check(lib().rtw_encode_rgb8_device(C.c_void_p(d_image), pixels, C.c_void_p(d_rgb8), C.c_void_p(stream_ptr or 0)))
+
+
 def device_count() -> int:
     n = C.c_int()
     check(lib().rtw_device_count(C.byref(n)))

@@ -119,3 +119,23 @@ def test_progress_callback_reports_and_keeps_bits(worlds):
     assert all(t == total for _, t in seen)
     assert all(a[0] <= b[0] for a, b in zip(seen, seen[1:]))
     assert_bit_identical(img, R.render(size, 1, 48, 50, world, seed=5), "progress render")
+
+
+def test_device_encoder_matches_host():
+    """rtw_encode_rgb8_device (the device to_rgb8_gamma2) == the host encoder, byte for byte, on
+    random and special values (NaN, infinities, negatives, the 255 boundary)."""
+    import torch
+
+    from raytracinginaweekend_amd.image_io import to_rgb8_gamma2
+    from raytracinginaweekend_amd.rendering import encode_rgb8_device
+
+    rng = np.random.default_rng(5)
+    special = np.array([0.0, -0.0, 1.0, 0.25, 1e30, -1.0, np.nan, np.inf, -np.inf, (255.0 / 256) ** 2,
+                        (254.999 / 256) ** 2], np.float32)
+    x = np.concatenate([special, rng.random(30000).astype(np.float32), rng.lognormal(0, 3, 3001).astype(np.float32)])
+    x = x[: len(x) // 3 * 3]
+    d = torch.from_numpy(x).to("cuda:0")
+    out = torch.zeros(len(x), dtype=torch.uint8, device="cuda:0")
+    encode_rgb8_device(d.data_ptr(), len(x) // 3, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), to_rgb8_gamma2(x.reshape(-1, 3)).ravel())
