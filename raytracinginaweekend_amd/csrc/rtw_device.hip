@@ -78,16 +78,17 @@ struct WorldConst {
 };
 
 // On-device tuning of the dynamic-fetch threshold, kept per world.  A launch that finds chosen == 0
-// runs exploration epochs of RTW_TUNE_EPOCH_TICKS (100 MHz clock): candidate cand[e] (mirrored,
-// a..f f..a) in epoch e, recording the work-item counter at each epoch start; after the last
-// epoch every wave derives the same winner (most items handed out per candidate) and publishes it.
+// and has room for it explores candidates over epochs of `tune_items` work items -- whole passes
+// over the launch's pixel slots, so every epoch renders the same pixels (other samples) and epoch
+// times compare like for like.  Epoch 0 warms up; epoch j = 1..EPOCHS runs candidate
+// cand[j-1] (mirrored, a..f f..a); the wave whose refill hands out the first item of an epoch
+// records the 100 MHz clock.  Once the last epoch has ended every wave derives the same winner
+// (least time over its two epochs) and publishes it for the world's later launches.
 #define RTW_TUNE_NCAND 6
 #define RTW_TUNE_EPOCHS (2 * RTW_TUNE_NCAND)
-#define RTW_TUNE_EPOCH_TICKS 400000ull  // 4 ms
 struct TuneState {
-    unsigned long long t0;                          // clock at the first refill (~0: unset)
-    unsigned long long start[RTW_TUNE_EPOCHS + 1];  // work-item counter at each epoch start
-    int chosen;                                     // the world's threshold once decided (0: not yet)
+    unsigned long long tb[RTW_TUNE_EPOCHS + 1];  // clock when item (j + 1) * tune_items was handed out
+    int chosen;                                  // the world's threshold once decided (0: not yet)
 };
 __constant__ const int kTuneCand[RTW_TUNE_NCAND] = {12, 16, 24, 32, 40, 48};
 
@@ -122,6 +123,7 @@ struct KArgs {
     float* out;
     unsigned long long* stats; // 13 counters (stats variant only)
     TuneState* tune;          // in-frame threshold tuning, or null
+    uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -350,6 +352,10 @@ __device__ __forceinline__ bool geom_t(const DWorld& w, int kind, int idx, const
     return tri_test(load_tri(w.tri_fast, idx), r, ts, te, t);
 }
 
+// device-only leaf_info.w bit (above the RTW_LEAF_* flags): the leaf's material samples an image
+// texture somewhere in its texture tree, so its hit record needs uv
+#define RTW_DLEAF_UV (1u << 16)
+
 // ---------------------------------------------------------------------------------------------
 // leaf wrappers (hittable.rs:234-244, 271-292; transformations.rs:37-111)
 // ---------------------------------------------------------------------------------------------
@@ -449,9 +455,16 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         const float4 s = w.spheres[idx];
         const V3 pos = at(rr, t);
         const V3 sn = divs(sub(pos, v3(s.x, s.y, s.z)), s.w);
-        const float theta = d_acosf(sn.y);  // vec3.rs:241-249
-        const float phi = d_atan2f(-sn.z, sn.x) + F32_PI;
-        from_ray(h, rr, pos, sn, phi / F32_TAU, theta / F32_PI);
+        // uv (vec3.rs:241-249) only reaches the image through an image texture; a pure function
+        // of the normal, so skipping it where no image texture can read it changes nothing
+        float u = 0.0f, v = 0.0f;
+        if (flags & RTW_DLEAF_UV) {
+            const float theta = d_acosf(sn.y);
+            const float phi = d_atan2f(-sn.z, sn.x) + F32_PI;
+            u = phi / F32_TAU;
+            v = theta / F32_PI;
+        }
+        from_ray(h, rr, pos, sn, u, v);
     } else if (kind == RTW_GEOM_RECT) {  // rect_geometry.rs:37-55
         const RectG g = load_rect(w, idx);
         int p0, p1, n;
@@ -914,10 +927,14 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // struct is read through a pointer; left in the loop it becomes a dependent global load)
     const float4* tri_fast = uniform_ptr(w.tri_fast);
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
+    // The LDS section offsets are held in VGPRs (opaque copies): as SGPRs they compete with the
+    // loop's exec masks and get spilled to VGPR lanes, costing a v_readlane per node step.
+    int32_t off_b = n_nodes, off_f = 2 * n_nodes, off_k = 2 * (2 * n_nodes + n_leaves);
+    if (LDS_SCENE) asm volatile("" : "+v"(off_b), "+v"(off_f), "+v"(off_k));
     const float4* nodes_a = LDS_SCENE ? smem : w.node_a;
-    const float4* nodes_b = LDS_SCENE ? smem + n_nodes : w.node_b;
-    const float4* fast = LDS_SCENE ? smem + 2 * n_nodes : w.leaf_fast;
-    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem + 2 * n_nodes + n_leaves) : w.node_km;
+    const float4* nodes_b = LDS_SCENE ? smem + off_b : w.node_b;
+    const float4* fast = LDS_SCENE ? smem + off_f : w.leaf_fast;
+    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem) + off_k : w.node_km;
     int32_t* stack = reinterpret_cast<int32_t*>(smem + (LDS_SCENE ? 2 * n_nodes + n_leaves + (n_nodes + 1) / 2 : 0)) +
                      threadIdx.x;
     Stats st;
@@ -1069,55 +1086,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     };
 
     int32_t trace_min = A.trace_min;  // this wave's dynamic-fetch threshold (tuned below)
-    bool tuned = A.tune == nullptr;
+    bool tuned = true;
+    if (A.tune) {
+        const int ch = __hip_atomic_load(&A.tune->chosen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ch > 0) trace_min = ch;
+        else tuned = A.tune_items == 0;
+    }
     for (;;) {
-        if (!tuned) {  // wave-uniform: scalar loads and a leader's atomics
-            const int ch = __hip_atomic_load(&A.tune->chosen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (ch > 0) {
-                trace_min = ch;
-                tuned = true;
-            } else {
-                const bool leader = lane == __ffsll((long long)__ballot(1)) - 1;
-                const unsigned long long now = wall_clock64();
-                unsigned long long t0 = __hip_atomic_load(&A.tune->t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (t0 == ~0ull) {
-                    if (leader) atomicCAS(&A.tune->t0, ~0ull, now);
-                    t0 = now;
-                }
-                const unsigned long long e = (now - t0) / RTW_TUNE_EPOCH_TICKS;
-                if (e <= (unsigned long long)RTW_TUNE_EPOCHS) {
-                    if (leader &&
-                        __hip_atomic_load(&A.tune->start[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ~0ull)
-                        atomicCAS(&A.tune->start[e], ~0ull,
-                                  __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    trace_min = e < RTW_TUNE_EPOCHS
-                                    ? kTuneCand[e < RTW_TUNE_NCAND ? e : RTW_TUNE_EPOCHS - 1 - e]
-                                    : A.trace_min;
-                } else {
-                    unsigned long long st[RTW_TUNE_EPOCHS + 1];
-                    bool ok = true;
-                    for (int i = 0; i <= RTW_TUNE_EPOCHS; ++i) {
-                        st[i] = __hip_atomic_load(&A.tune->start[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok = ok && st[i] != ~0ull && (i == 0 || st[i] >= st[i - 1]);
-                    }
-                    int best = A.trace_min;
-                    if (ok) {
-                        unsigned long long best_n = 0;
-                        for (int c = 0; c < RTW_TUNE_NCAND; ++c) {
-                            const unsigned long long n =
-                                (st[c + 1] - st[c]) + (st[RTW_TUNE_EPOCHS - c] - st[RTW_TUNE_EPOCHS - 1 - c]);
-                            if (c == 0 || n > best_n) {
-                                best_n = n;
-                                best = kTuneCand[c];
-                            }
-                        }
-                        if (leader) atomicCAS(&A.tune->chosen, 0, best);
-                    }
-                    trace_min = best;
-                    tuned = ok;
-                }
-            }
-        }
         // 1. lanes without a pixel take the next ones (one atomic per wave per round)
         bool out_of_work = false;
         for (;;) {
@@ -1127,6 +1102,40 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             unsigned long long base = 0;
             if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
             base = __shfl(base, leader);
+            if (!tuned) {  // wave-uniform; the batch holding an epoch's first item stamps its start
+                const uint64_t E = A.tune_items;
+                const uint64_t j = (base + E - 1) / E;
+                if (lane == leader && j >= 1 && j <= RTW_TUNE_EPOCHS + 1 && j * E < base + (uint64_t)__popcll(m))
+                    __hip_atomic_store(&A.tune->tb[j - 1], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t e = base / E;
+                if (e == 0) {
+                    trace_min = A.trace_min;
+                } else if (e <= RTW_TUNE_EPOCHS) {
+                    const int i = (int)e - 1;
+                    trace_min = kTuneCand[i < RTW_TUNE_NCAND ? i : RTW_TUNE_EPOCHS - 1 - i];
+                } else {
+                    unsigned long long tb[RTW_TUNE_EPOCHS + 1];
+                    bool ok = true;
+                    for (int k = 0; k <= RTW_TUNE_EPOCHS; ++k) {
+                        tb[k] = __hip_atomic_load(&A.tune->tb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = ok && tb[k] != ~0ull;
+                    }
+                    trace_min = A.trace_min;
+                    if (ok) {  // epoch j (1-based) lasted tb[j] - tb[j-1]
+                        unsigned long long best_t = 0;
+                        for (int c = 0; c < RTW_TUNE_NCAND; ++c) {
+                            const unsigned long long t = (tb[c + 1] - tb[c]) +
+                                                         (tb[RTW_TUNE_EPOCHS - c] - tb[RTW_TUNE_EPOCHS - 1 - c]);
+                            if (c == 0 || t < best_t) {
+                                best_t = t;
+                                trace_min = kTuneCand[c];
+                            }
+                        }
+                        if (lane == leader) atomicCAS(&A.tune->chosen, 0, trace_min);
+                        tuned = true;
+                    }
+                }
+            }
             if (T.phase == PH_PIXEL) {
                 const unsigned long long below = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
                 const uint64_t item = base + (uint64_t)__popcll(below);
@@ -1350,6 +1359,26 @@ struct Layout {
     }
 };
 
+// does material m's texture tree (checker children followed, as texture_sample does) hold an
+// image texture?  Conservative on cycles / deep chains (the device gives up after 64 steps).
+bool material_reads_uv(const rtw_world* w, int m) {
+    const rtw_material& M = w->materials[m];
+    if (M.kind == RTW_MAT_DIELECTRIC) return false;
+    std::vector<int> todo{M.texture};
+    for (int steps = 0; !todo.empty(); ++steps) {
+        if (steps > 4096) return true;
+        const int t = todo.back();
+        todo.pop_back();
+        const rtw_texture& T = w->textures[t];
+        if (T.kind == RTW_TEX_IMAGE) return true;
+        if (T.kind == RTW_TEX_CHECKER) {
+            todo.push_back(T.even);
+            todo.push_back(T.odd);
+        }
+    }
+    return false;
+}
+
 int check_world(const rtw_world* w, int* depth_out) {
     if (!w) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null world");
     if (w->leaf_count < 1) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "world has no leaves");
@@ -1499,7 +1528,8 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     std::vector<float4> lx((size_t)w->leaf_count * 3);
     for (int i = 0; i < w->leaf_count; ++i) {
         const rtw_leaf& l = w->leaves[i];
-        li[(size_t)i] = make_int4(l.geom_kind, l.geom_index, l.material, (int)l.flags);
+        li[(size_t)i] = make_int4(l.geom_kind, l.geom_index, l.material,
+                                  (int)(l.flags | (material_reads_uv(w, l.material) ? RTW_DLEAF_UV : 0u)));
         lx[3 * (size_t)i] = make_float4(l.neg_inv_density, l.offset[0], l.offset[1], l.offset[2]);
         lx[3 * (size_t)i + 1] = make_float4(l.y_sin, l.y_cos, l.velocity[0], l.velocity[1]);
         lx[3 * (size_t)i + 2] = make_float4(l.velocity[2], 0.0f, 0.0f, 0.0f);
@@ -1747,6 +1777,17 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const int64_t want = (int64_t)((A.items + RTW_BLOCK - 1) / RTW_BLOCK);
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per_cu * g->cus));
     HIP_TRY(hipMemsetAsync(A.queue, 0, sizeof(unsigned long long), stream));
+    // tuning epochs: whole passes over the slots, at least 4x the resident lanes in items (the
+    // items in flight blur epoch boundaries); explore only if warm-up + all epochs + one more fit
+    A.tune_items = 0;
+    if (A.tune && A.total > 0) {
+        const uint64_t lanes = (uint64_t)blocks * RTW_BLOCK;
+        const uint64_t E = (uint64_t)A.total * ((4 * lanes + A.total - 1) / A.total);
+        if (A.items_big >= (uint64_t)(RTW_TUNE_EPOCHS + 2) * E) {
+            A.tune_items = E;
+            HIP_TRY(hipMemsetAsync(A.tune->tb, 0xFF, sizeof(A.tune->tb), stream));
+        }
+    }
     if (stats) {
         if (lds_scene) hipLaunchKernelGGL((render_kernel<true, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
         else hipLaunchKernelGGL((render_kernel<true, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
@@ -1811,13 +1852,10 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
     A.colors = g->colors;
     A.chunk = chunk;
     // In-frame tuning of the dynamic-fetch threshold (TuneState): until a world has chosen one,
-    // each render launch explores candidates over timed epochs on the device.  RTW_TRACE_MIN
+    // each render launch with room for it explores candidates over pass-aligned epochs.  RTW_TRACE_MIN
     // fixes the threshold instead.
     A.tune = nullptr;
-    if (!stats && !std::getenv("RTW_TRACE_MIN")) {
-        A.tune = g->tune;
-        HIP_TRY(hipMemsetAsync(g->tune, 0xFF, offsetof(TuneState, chosen), stream));
-    }
+    if (!stats && !std::getenv("RTW_TRACE_MIN")) A.tune = g->tune;
     HIP_TRY(hipMemsetAsync(g->queue, 0, RTW_QUEUE_SLOTS * sizeof(unsigned long long), stream));
     int launch = 0;
     for (uint32_t s0 = 0; s0 < A.spp; s0 += (uint32_t)per_launch, ++launch) {
