@@ -287,6 +287,13 @@ RTW_API int rtw_encode_rgb8_device(const float* d_image, int64_t pixels, uint8_t
 RTW_API int rtw_device_eval_scalar(int device, int fn, const float* a, const float* b, int64_t n,
                                    float* out);
 
+/* Device self-test of the traversal's node step (Aabb::hit_cond, aabb.rs:65-78, AND the proximity
+ * cull): for each i, box[6i..] = min xyz, max xyz; ray[6i..] = origin xyz, direction xyz;
+ * range[2i..] = t_start, t_end; km[2i..] = the node's cull constants; mk_world as computed at upload
+ * (1: node coordinates admit the per-ray exact-division guard).  out[i] = 1 if the node passes. */
+RTW_API int rtw_device_eval_node_pass(int device, const float* box, const float* ray, const float* range,
+                                      const float* km, int32_t mk_world, int64_t n, int32_t* out);
+
 /* ---- host scene construction ------------------------------------------------------------- */
 typedef struct rtw_builder rtw_builder;         /* WorldBuilder + arena (world_builder.rs:7-14) */
 typedef struct rtw_world_handle rtw_world_handle; /* owns a finished flat World */

@@ -58,6 +58,8 @@ def lib():
         L.rtw_oracle_eval_scalar.restype = C.c_int
         L.rtw_oracle_eval_scalar.argtypes = [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int64,
                                              C.POINTER(C.c_float)]
+        L.rtw_oracle_node_pass.restype = C.c_int
+        L.rtw_oracle_node_pass.argtypes = [C.POINTER(C.c_float)] * 4 + [C.c_int64, C.POINTER(C.c_int32)]
         _lib = L
     return _lib
 

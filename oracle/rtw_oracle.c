@@ -1024,3 +1024,24 @@ RTW_API int rtw_oracle_eval_scalar(int fn, const float* a, const float* b, int64
     }
     return RTW_OK;
 }
+
+RTW_API int rtw_oracle_node_pass(const float* box, const float* ray, const float* range, const float* km, int64_t n,
+                                 int32_t* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        rtw_bvh_node nd;
+        memset(&nd, 0, sizeof(nd));
+        for (int k = 0; k < 3; ++k) {
+            nd.min[k] = box[6 * i + k];
+            nd.max[k] = box[6 * i + 3 + k];
+        }
+        Ray r;
+        memset(&r, 0, sizeof(r));
+        for (int k = 0; k < 3; ++k) {
+            r.origin.e[k] = ray[6 * i + k];
+            r.dir.e[k] = ray[6 * i + 3 + k];
+        }
+        const float ts = range[2 * i], te = range[2 * i + 1];
+        out[i] = aabb_hit_cond(&nd, &r, ts, te) && cull_pass(km + 2 * i, 0, &nd, &r, ts, te);
+    }
+    return RTW_OK;
+}

@@ -59,6 +59,11 @@ RTW_API int rtw_oracle_ray_color(const rtw_world* w, const float origin[3], cons
 /* Scalar spec evaluation on the host (for the device self-test comparison). */
 RTW_API int rtw_oracle_eval_scalar(int fn, const float* a, const float* b, int64_t n, float* out);
 
+/* The reference's Aabb::hit_cond AND the product's proximity cull (same layout as
+ * rtw_device_eval_node_pass; the checker for the device's node step). */
+RTW_API int rtw_oracle_node_pass(const float* box, const float* ray, const float* range, const float* km, int64_t n,
+                                 int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -252,6 +252,10 @@ _SIGS = {
         C.c_int,
         [C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_float)],
     ),
+    "rtw_device_eval_node_pass": (
+        C.c_int,
+        [C.c_int] + [C.POINTER(C.c_float)] * 4 + [C.c_int32, C.c_int64, C.POINTER(C.c_int32)],
+    ),
     "rtw_rng_from_seed": (_P, [C.POINTER(C.c_uint8)]),
     "rtw_rng_free": (None, [_P]),
     "rtw_rng_gen_f32": (C.c_float, [_P]),

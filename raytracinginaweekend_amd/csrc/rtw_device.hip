@@ -123,6 +123,7 @@ struct KArgs {
     float* out;
     unsigned long long* stats; // 13 counters (stats variant only)
     TuneState* tune;          // in-frame threshold tuning, or null
+    int32_t mk_world;         // node coordinates admit the per-ray exact-division guard (ray_pre)
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
 };
 
@@ -522,16 +523,22 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
 // ---------------------------------------------------------------------------------------------
 // Exact f32 division by a ray-direction component d with y = RN(1/d) precomputed per ray
 // (Markstein): q = RN(a*y); r = fma(-d, q, a) (exact); q' = RN(q + r*y) == RN(a/d), provided
-// no underflow/overflow: the caller guarantees 2^-60 <= |d| <= 2, 2^-40 <= |a| <= 2^40 (the
-// upper bound holds by construction: world coordinates are bounded by 2^30 at upload)
-// (tests/native/markstein_check.c checks every divisor significand under these guards).
+// 2^-60 <= |d| <= 2 and 2^-84 <= |a| <= 2^40, or a = 0 (then q' is a zero whose sign may differ
+// from a/d's; the slab test only compares quotients, so no decision sees it).
+// (tests/native/markstein_check.c checks every divisor significand under these guards.)
+// The guards hold per ray, not per node: a = RN(c - o) for a node coordinate c and an origin
+// component o.  If o = 0, a = c.  If |o| >= 2^-60 and c != o, |c - o| >= 2^-84 (the difference of
+// two distinct floats is at least the finer one's ulp, or at least |o|/2).  So when every node
+// coordinate is 0 or at least 2^-60 in magnitude (checked at upload: `mk_world`) and so is every
+// origin component, each |a| is 0 or >= 2^-84; |a| <= 2^31 since coordinates are bounded by 2^30
+// at upload.
 #define RTW_MK_DMIN 0x1p-60f
-#define RTW_MK_AMIN 0x1p-40f
-#define RTW_MK_AMAX 0x1p40f
+#define RTW_MK_CMIN 0x1p-60f
 __device__ __forceinline__ float mk_div(float a, float d, float y) {
     const float q = a * y;
     return __builtin_fmaf(__builtin_fmaf(-d, q, a), y, q);
 }
+__device__ __forceinline__ bool mk_coord_ok(float c) { return c == 0.0f || __builtin_fabsf(c) >= RTW_MK_CMIN; }
 
 // One axis of Aabb::hit_cond (aabb.rs:65-78): (t0, t1) = minmax(qa, qb) (math.rs:35-41: `a < b`
 // else swapped, so a NaN lands in t1 position of qa), tmin = max(t0, ts), tmax = min(t1, te) with
@@ -549,14 +556,16 @@ struct RayPre {  // per-ray constants of the slab test
     V3 inv;
     bool fast;
 };
-__device__ __forceinline__ RayPre ray_pre(const Ray& r) {
+// mk_world: every node coordinate is 0 or >= 2^-60 in magnitude (rtw_world_upload)
+__device__ __forceinline__ RayPre ray_pre(const Ray& r, bool mk_world) {
     RayPre p;
     p.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
                                     __builtin_fabsf(r.d.z));
     const float M = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
                                     __builtin_fabsf(r.d.z));
-    p.fast = (m >= RTW_MK_DMIN) && (M <= 2.0f);
+    p.fast = mk_world && (m >= RTW_MK_DMIN) && (M <= 2.0f) && mk_coord_ok(r.o.x) && mk_coord_ok(r.o.y) &&
+             mk_coord_ok(r.o.z);
     return p;
 }
 
@@ -567,29 +576,36 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
     const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
-    const float lo = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fabsf(a0), __builtin_fabsf(b0)),
-                                                     __builtin_fminf(__builtin_fabsf(a1), __builtin_fabsf(b1))),
-                                     __builtin_fminf(__builtin_fabsf(a2), __builtin_fabsf(b2)));
     // D = sum_i |a_i| + |b_i| (>= sum_i max(|a_i|, |b_i|) >= |o - x|; abs-modifier adds, no max)
     const float dsum = ((__builtin_fabsf(a0) + __builtin_fabsf(b0)) + (__builtin_fabsf(a1) + __builtin_fabsf(b1))) +
                        (__builtin_fabsf(a2) + __builtin_fabsf(b2));
-    // |a| <= 2^32 always: rtw_world_upload bounds every coordinate by 2^30 (check_world)
-    float qa0, qb0, qa1, qb1, qa2, qb2;
-    if (__builtin_expect(rp.fast && lo >= RTW_MK_AMIN, 1)) {
-        qa0 = mk_div(a0, r.d.x, rp.inv.x);
-        qb0 = mk_div(b0, r.d.x, rp.inv.x);
-        qa1 = mk_div(a1, r.d.y, rp.inv.y);
-        qb1 = mk_div(b1, r.d.y, rp.inv.y);
-        qa2 = mk_div(a2, r.d.z, rp.inv.z);
-        qb2 = mk_div(b2, r.d.z, rp.inv.z);
-    } else {
-        qa0 = a0 / r.d.x;
-        qb0 = b0 / r.d.x;
-        qa1 = a1 / r.d.y;
-        qb1 = b1 / r.d.y;
-        qa2 = a2 / r.d.z;
-        qb2 = b2 / r.d.z;
+    const float delta = rtw_cull_delta(km.x, km.y, dsum);
+    if (__builtin_expect(rp.fast, 1)) {
+        const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
+        const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
+        const float qa2 = mk_div(a2, r.d.z, rp.inv.z), qb2 = mk_div(b2, r.d.z, rp.inv.z);
+        // Finite quotients (|a| <= 2^31, |d| >= 2^-60): no NaN, so Rust's minmax is min / max
+        // (equal operands, +-0 included, only meet comparisons).
+        const float t00 = __builtin_fminf(qa0, qb0), t10 = __builtin_fmaxf(qa0, qb0);
+        const float t01 = __builtin_fminf(qa1, qb1), t11 = __builtin_fmaxf(qa1, qb1);
+        const float t02 = __builtin_fminf(qa2, qb2), t12 = __builtin_fmaxf(qa2, qb2);
+        const float t1min = __builtin_fminf(__builtin_fminf(t10, t11), t12);
+        const float t0max = __builtin_fmaxf(__builtin_fmaxf(t00, t01), t02);
+        const int hit_cond = (int)(te > ts) & (int)!(t1min <= ts) & (int)!(te <= t0max) & (int)(qa0 != qb0) &
+                             (int)(qa1 != qb1) & (int)(qa2 != qb2);
+        // Given hit_cond, the cull's [max(ts, t0_i - w_i), min(te, t1_j + w_j)] is non-empty iff
+        // max_i (t0_i - w_i) <= min_j (t1_j + w_j): ts <= te, ts < t1_j <= t1_j + w_j and
+        // t0_i - w_i <= t0_i < te hold already (w_i >= 0).  A NaN delta (k = inf, D = 0, so every
+        // a_i = b_i = 0 and hit_cond fails) passes, as rtw_cull_axis's NaN-dropping bounds do.
+        const float w0 = delta * __builtin_fabsf(rp.inv.x), w1 = delta * __builtin_fabsf(rp.inv.y),
+                    w2 = delta * __builtin_fabsf(rp.inv.z);
+        const float lo = __builtin_fmaxf(__builtin_fmaxf(t00 - w0, t01 - w1), t02 - w2);
+        const float hi = __builtin_fminf(__builtin_fminf(t10 + w0, t11 + w1), t12 + w2);
+        return hit_cond & (int)!(lo > hi);
     }
+    const float qa0 = a0 / r.d.x, qb0 = b0 / r.d.x;
+    const float qa1 = a1 / r.d.y, qb1 = b1 / r.d.y;
+    const float qa2 = a2 / r.d.z, qb2 = b2 / r.d.z;
     // minmax per axis (math.rs:35-41: `a < b` else swapped)
     const bool l0 = qa0 < qb0, l1 = qa1 < qb1, l2 = qa2 < qb2;
     const float t00 = l0 ? qa0 : qb0, t10 = l0 ? qb0 : qa0;
@@ -602,7 +618,6 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
     const float t0max = __builtin_fmaxf(__builtin_fmaxf(t00, t01), t02);
     const int hit_cond = (int)(te > ts) & (int)!(t1min <= ts) & (int)!(te <= t0max) & (int)(qa0 != qb0) &
                          (int)(qa1 != qb1) & (int)(qa2 != qb2);
-    const float delta = rtw_cull_delta(km.x, km.y, dsum);
     float clo = ts, chi = te;
     rtw_cull_axis(t00, t10, delta * __builtin_fabsf(rp.inv.x), &clo, &chi);
     rtw_cull_axis(t01, t11, delta * __builtin_fabsf(rp.inv.y), &clo, &chi);
@@ -1176,7 +1191,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
         if (fresh) {
             fresh = false;
-            const RayPre rp = ray_pre(T.ray);
+            const RayPre rp = ray_pre(T.ray, A.mk_world != 0);
             T.inv = rp.inv;
             T.fast = rp.fast ? 1 : 0;
             T.node = w.root;
@@ -1328,6 +1343,23 @@ __global__ void eval_scalar_kernel(int fn, const float* a, const float* b, int64
     out[i] = r;
 }
 
+__global__ void eval_node_pass_kernel(const float* box, const float* ray, const float* range, const float* km,
+                                      int32_t mk_world, int64_t n, int32_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* b = box + 6 * i;
+    const float* r = ray + 6 * i;
+    Ray R;
+    R.o = v3(r[0], r[1], r[2]);
+    R.d = v3(r[3], r[4], r[5]);
+    R.time = 0.0f;
+    const RayPre rp = ray_pre(R, mk_world != 0);
+    out[i] = node_pass(make_float4(b[0], b[1], b[2], b[3]), make_float4(b[4], b[5], 0.0f, 0.0f),
+                       make_float2(km[2 * i], km[2 * i + 1]), R, rp, range[2 * i], range[2 * i + 1])
+                 ? 1
+                 : 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -1465,6 +1497,7 @@ struct rtw_gpu_world {
     DWorld w{};
     const DWorld* wdev = nullptr;
     int32_t node_count = 0, leaf_count = 0, depth = 1;
+    int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int cus = 0;
     int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
     TuneState* tune = nullptr;  // in-frame threshold tuning state
@@ -1673,6 +1706,11 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->node_count = w->node_count;
     g->leaf_count = w->leaf_count;
     g->depth = std::max(1, depth);
+    g->mk_world = 1;
+    for (int i = 0; i < w->node_count; ++i)
+        for (int k = 0; k < 3; ++k)
+            for (float c : {w->nodes[i].min[k], w->nodes[i].max[k]})
+                if (!(c == 0.0f || std::fabs(c) >= 0x1p-60f)) g->mk_world = 0;
     (void)hipDeviceGetAttribute(&g->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (g->cus <= 0) g->cus = 256;
     {
@@ -1746,6 +1784,7 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.total = (uint32_t)(owned * tw * th);
     A.node_count = g->node_count;
     A.leaf_count = g->leaf_count;
+    A.mk_world = g->mk_world;
     A.queue = g->queue;
     A.wdev = g->wdev;
     A.trace_min = 32;
@@ -2081,6 +2120,36 @@ extern "C" RTW_API int rtw_encode_rgb8_device(const float* d_image, int64_t pixe
     hipLaunchKernelGGL(encode_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_image,
                        pixels, d_rgb8);
     HIP_TRY(hipGetLastError());
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, const float* ray, const float* range,
+                                                 const float* km, int32_t mk_world, int64_t n, int32_t* out) {
+    if (!box || !ray || !range || !km || !out || n < 0) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device");
+    HIP_TRY(hipSetDevice(device));
+    if (n == 0) return RTW_OK;
+    float *db = nullptr, *dr = nullptr, *dg = nullptr, *dk = nullptr;
+    int32_t* dout = nullptr;
+    HIP_TRY(hipMalloc(&db, (size_t)n * 6 * sizeof(float)));
+    HIP_TRY(hipMalloc(&dr, (size_t)n * 6 * sizeof(float)));
+    HIP_TRY(hipMalloc(&dg, (size_t)n * 2 * sizeof(float)));
+    HIP_TRY(hipMalloc(&dk, (size_t)n * 2 * sizeof(float)));
+    HIP_TRY(hipMalloc(&dout, (size_t)n * sizeof(int32_t)));
+    HIP_TRY(hipMemcpy(db, box, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dr, ray, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dg, range, (size_t)n * 2 * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dk, km, (size_t)n * 2 * sizeof(float), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(eval_node_pass_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, db, dr, dg, dk, mk_world,
+                       n, dout);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(out, dout, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    (void)hipFree(db);
+    (void)hipFree(dr);
+    (void)hipFree(dg);
+    (void)hipFree(dk);
+    (void)hipFree(dout);
     return RTW_OK;
 }
 
