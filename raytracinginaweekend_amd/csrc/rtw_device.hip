@@ -30,14 +30,14 @@
 #include "rtw_common.h"
 
 #ifndef RTW_BLOCK
-#define RTW_BLOCK 512   // 8 waves; 2 blocks per CU at <= 128 VGPRs -> 4 waves per SIMD
+#define RTW_BLOCK 1024  // 16 waves: one block per CU at <= 128 VGPRs -> 4 waves per SIMD, one LDS scene copy per CU
 #endif
 #ifndef RTW_MIN_WAVES_PER_SIMD
 #define RTW_MIN_WAVES_PER_SIMD 4
 #endif
 #define RTW_STACK 32    // per-lane traversal stack (LDS), >= the BVH depth (checked at upload)
 #ifndef RTW_LDS_SCENE_MAX
-#define RTW_LDS_SCENE_MAX (96 * 1024)  // nodes + leaf records staged in LDS when they fit
+#define RTW_LDS_SCENE_MAX (160 * 1024)  // LDS bytes per block the scene (+ stack) may take
 #endif
 
 namespace {
@@ -102,7 +102,7 @@ struct KArgs {
     int32_t tile_w, tile_h, tiles_x, n_tiles;
     int32_t part_index, part_count;
     uint32_t total;          // pixel slots in this partition (owned tiles * tile_w * tile_h)
-    int32_t node_count, leaf_count;
+    int32_t node_count, leaf_count, tri_count;
     unsigned long long* queue; // work-item counter (zeroed before each launch)
     // one launch renders samples [s_begin, s_end) of every slot as work items of `chunk`
     // consecutive samples (item = chunk index * total + slot); each finished sample's colour goes
@@ -934,13 +934,18 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
     }
 }
 
-template <bool STATS, bool LDS_SCENE>
+// LDS modes of the render kernel: 0 scene in HBM, 1 nodes + leaf records + cull constants in LDS,
+// 2 also the plain-triangle records (tri_fast).  LDS layout: [node_a n][node_b n][leaf_fast L]
+// [km ceil(n/2)][tri_fast 4T (mode 2)][stack depth x BLOCK]
+template <bool STATS, int LDS>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
-                                      int32_t n_leaves, unsigned long long* dbg) {
+                                      int32_t n_leaves, int32_t n_tris, unsigned long long* dbg) {
+    constexpr bool LDS_SCENE = LDS >= 1;
     const DWorld& w = *wp;
     // the plain-triangle records' base, loaded once per call into scalar registers (the world
     // struct is read through a pointer; left in the loop it becomes a dependent global load)
-    const float4* tri_fast = uniform_ptr(w.tri_fast);
+    const int32_t tri_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
+    const float4* tri_fast = LDS == 2 ? smem + tri_off : uniform_ptr(w.tri_fast);
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
     // The LDS section offsets are held in VGPRs (opaque copies): as SGPRs they compete with the
     // loop's exec masks and get spilled to VGPR lanes, costing a v_readlane per node step.
@@ -950,7 +955,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     const float4* nodes_b = LDS_SCENE ? smem + off_b : w.node_b;
     const float4* fast = LDS_SCENE ? smem + off_f : w.leaf_fast;
     const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem) + off_k : w.node_km;
-    int32_t* stack = reinterpret_cast<int32_t*>(smem + (LDS_SCENE ? 2 * n_nodes + n_leaves + (n_nodes + 1) / 2 : 0)) +
+    int32_t* stack = reinterpret_cast<int32_t*>(smem + (LDS_SCENE ? tri_off + (LDS == 2 ? 4 * n_tris : 0) : 0)) +
                      threadIdx.x;
     Stats st;
     if (STATS)
@@ -1045,8 +1050,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     return T;
 }
 
-template <bool STATS, bool LDS_SCENE>
+template <bool STATS, int LDS>
 __device__ __forceinline__ void render_body(const KArgs& A) {
+    constexpr bool LDS_SCENE = LDS >= 1;
     // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
     // per node)] [stack: depth x BLOCK]
     const DWorld& w = A.w;
@@ -1058,6 +1064,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
         float2* km = reinterpret_cast<float2*>(smem + 2 * A.node_count + A.leaf_count);
         for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = w.node_km[i];
+        if (LDS == 2) {
+            float4* tris = smem + 2 * A.node_count + A.leaf_count + (A.node_count + 1) / 2;
+            for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[i] = w.tri_fast[i];
+        }
         __syncthreads();
     }
     Stats st;
@@ -1202,7 +1212,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
 
         // 3. traversal (hittable.rs:429-473)
-        T = traverse<STATS, LDS_SCENE>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, A.leaf_count,
+        T = traverse<STATS, LDS>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, A.leaf_count,
+                                 A.tri_count,
                                        STATS ? A.stats + ST_COUNT : nullptr);
         if (STATS) {
             c_mark = clock64();
@@ -1264,9 +1275,9 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     }
 }
 
-template <bool STATS, bool LDS_SCENE>
+template <bool STATS, int LDS>
 __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
-    render_body<STATS, LDS_SCENE>(A);
+    render_body<STATS, LDS>(A);
 }
 // Per slot: sum += colour of each sample of this launch, in sample order (the running sum of
 // earlier launches is carried in `running`); the last launch writes sum / spp (rendering.rs:179;
@@ -1497,9 +1508,11 @@ struct rtw_gpu_world {
     DWorld w{};
     const DWorld* wdev = nullptr;
     int32_t node_count = 0, leaf_count = 0, depth = 1;
+    int32_t tri_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int cus = 0;
     int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
+    int lds_cu = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerMultiprocessor
     TuneState* tune = nullptr;  // in-frame threshold tuning state
 };
 
@@ -1706,6 +1719,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->node_count = w->node_count;
     g->leaf_count = w->leaf_count;
     g->depth = std::max(1, depth);
+    g->tri_count = w->triangle_count;
     g->mk_world = 1;
     for (int i = 0; i < w->node_count; ++i)
         for (int k = 0; k < 3; ++k)
@@ -1717,6 +1731,8 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         int lm = 0;
         if (hipDeviceGetAttribute(&lm, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lm > 0)
             g->lds_max = lm;
+        if (hipDeviceGetAttribute(&lm, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) == hipSuccess && lm > 0)
+            g->lds_cu = lm;
     }
     e = hipMalloc(&g->tune, sizeof(TuneState));
     if (e == hipSuccess) e = hipMemset(g->tune, 0, sizeof(TuneState));
@@ -1785,6 +1801,7 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.node_count = g->node_count;
     A.leaf_count = g->leaf_count;
     A.mk_world = g->mk_world;
+    A.tri_count = g->tri_count;
     A.queue = g->queue;
     A.wdev = g->wdev;
     A.trace_min = 32;
@@ -1803,12 +1820,22 @@ enum LaunchKind { LK_RENDER, LK_STATS };
 int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const bool stats = kind == LK_STATS;
     const size_t scene_bytes = (size_t)(2 * g->node_count + g->leaf_count + (g->node_count + 1) / 2) * sizeof(float4);
+    const size_t tri_bytes = (size_t)g->tri_count * 4 * sizeof(float4);
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
-    const bool lds_scene = scene_bytes <= RTW_LDS_SCENE_MAX && scene_bytes + stack_bytes <= (size_t)g->lds_max;
-    const size_t lds = (lds_scene ? scene_bytes : 0) + stack_bytes;
-    const void* fn;
-    if (stats) fn = lds_scene ? (const void*)render_kernel<true, true> : (const void*)render_kernel<true, false>;
-    else fn = lds_scene ? (const void*)render_kernel<false, true> : (const void*)render_kernel<false, false>;
+    // a block may take its share of the CU's LDS at the kernel's target occupancy
+    // (RTW_MIN_WAVES_PER_SIMD waves on each of 4 SIMDs)
+    const int blocks_per_cu = std::max(1, (4 * RTW_MIN_WAVES_PER_SIMD * 64) / RTW_BLOCK);
+    const size_t cap = std::min({(size_t)RTW_LDS_SCENE_MAX, (size_t)g->lds_max, (size_t)g->lds_cu / blocks_per_cu});
+    int mode = 0;
+    if (g->tri_count > 0 && scene_bytes + tri_bytes + stack_bytes <= cap) mode = 2;
+    else if (scene_bytes + stack_bytes <= cap) mode = 1;
+    if (const char* e = std::getenv("RTW_LDS_MODE")) mode = std::min(mode, std::atoi(e));  // audits: cap the mode
+    const size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes : 0) + stack_bytes;
+    using KFn = void (*)(KArgs);
+    static const KFn fns[2][3] = {{render_kernel<false, 0>, render_kernel<false, 1>, render_kernel<false, 2>},
+                                  {render_kernel<true, 0>, render_kernel<true, 1>, render_kernel<true, 2>}};
+    const KFn kf = fns[stats ? 1 : 0][mode];
+    const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, RTW_BLOCK, lds));
@@ -1827,13 +1854,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
             HIP_TRY(hipMemsetAsync(A.tune->tb, 0xFF, sizeof(A.tune->tb), stream));
         }
     }
-    if (stats) {
-        if (lds_scene) hipLaunchKernelGGL((render_kernel<true, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
-        else hipLaunchKernelGGL((render_kernel<true, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
-    } else {
-        if (lds_scene) hipLaunchKernelGGL((render_kernel<false, true>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
-        else hipLaunchKernelGGL((render_kernel<false, false>), dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
-    }
+    hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
     HIP_TRY(hipGetLastError());
     return RTW_OK;
 }
