@@ -484,7 +484,11 @@ RTW_HD float rtw_sinf(float x) {
 /*   [ts, te] meets the box grown by delta, reusing hit_cond's slab quotients.                  */
 /* ------------------------------------------------------------------------------------------ */
 #define RTW_CULL_U 0x1p-24f
-RTW_HD float rtw_cull_delta(float k, float m, float d) { return (k * d) * d + ((64.0f * RTW_CULL_U) * d + m); }
+/* (k D + 64u) D + m, two fused steps (host and device round identically; any rounding of this
+ * bound is far inside the 9x safety factor of the cull analysis) */
+RTW_HD float rtw_cull_delta(float k, float m, float d) {
+    return __builtin_fmaf(__builtin_fmaf(k, d, 64.0f * RTW_CULL_U), d, m);
+}
 /* one axis: [t0 - w, t1 + w] narrows [lo, hi]; NaN operands are dropped (conservative) */
 RTW_HD void rtw_cull_axis(float t0, float t1, float w, float* lo, float* hi) {
     *lo = __builtin_fmaxf(*lo, t0 - w);
