@@ -1843,12 +1843,13 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const int64_t want = (int64_t)((A.items + RTW_BLOCK - 1) / RTW_BLOCK);
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per_cu * g->cus));
     HIP_TRY(hipMemsetAsync(A.queue, 0, sizeof(unsigned long long), stream));
-    // tuning epochs: whole passes over the slots, at least 4x the resident lanes in items (the
-    // items in flight blur epoch boundaries); explore only if warm-up + all epochs + one more fit
+    // tuning epochs: whole passes over the slots, at least 2x the resident lanes in items (the
+    // items in flight blur epoch boundaries; mirrored candidates cancel the blur's bias); explore
+    // only if warm-up + all epochs + one more fit (a 1080p x 512 spp frame split over 8 GPUs does)
     A.tune_items = 0;
     if (A.tune && A.total > 0) {
         const uint64_t lanes = (uint64_t)blocks * RTW_BLOCK;
-        const uint64_t E = (uint64_t)A.total * ((4 * lanes + A.total - 1) / A.total);
+        const uint64_t E = (uint64_t)A.total * ((2 * lanes + A.total - 1) / A.total);
         if (A.items_big >= (uint64_t)(RTW_TUNE_EPOCHS + 2) * E) {
             A.tune_items = E;
             HIP_TRY(hipMemsetAsync(A.tune->tb, 0xFF, sizeof(A.tune->tb), stream));
