@@ -125,6 +125,10 @@ struct KArgs {
     TuneState* tune;          // in-frame threshold tuning, or null
     int32_t mk_world;         // node coordinates admit the per-ray exact-division guard (ray_pre)
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
+    // work order by measured cost (render_frame): costlier tiles first, all their samples together
+    const uint32_t* tile_perm;  // tile rank -> local tile, null: chunk-major order
+    uint32_t* slot_cost;        // per slot: bounces of the deep (> 3 bounce) paths rendered there
+    uint32_t chunks;            // chunks per slot in this launch (tile_perm order)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -1170,10 +1174,22 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 } else {
                     const bool big = item < A.items_big;
                     const uint64_t rel = big ? item : item - A.items_big;
-                    const uint32_t ck = (uint32_t)(rel / A.total);
-                    const uint32_t c = (uint32_t)(rel - (uint64_t)ck * A.total);
-                    const int32_t lt = (int32_t)(c / (uint32_t)per_tile);
-                    const int32_t it = (int32_t)(c % (uint32_t)per_tile);
+                    uint32_t ck, c;
+                    int32_t lt, it;
+                    if (A.tile_perm) {  // tile-major in cost order: tile rank, chunk, pixel of the tile
+                        const uint64_t per_rank = (uint64_t)per_tile * A.chunks;
+                        const uint32_t g = (uint32_t)(rel / per_rank);
+                        const uint32_t wi = (uint32_t)(rel - (uint64_t)g * per_rank);
+                        ck = wi / (uint32_t)per_tile;
+                        it = (int32_t)(wi - ck * (uint32_t)per_tile);
+                        lt = (int32_t)A.tile_perm[g];
+                        c = (uint32_t)lt * (uint32_t)per_tile + (uint32_t)it;
+                    } else {  // chunk-major: pass after pass over the slots
+                        ck = (uint32_t)(rel / A.total);
+                        c = (uint32_t)(rel - (uint64_t)ck * A.total);
+                        lt = (int32_t)(c / (uint32_t)per_tile);
+                        it = (int32_t)(c % (uint32_t)per_tile);
+                    }
                     const int32_t tile = A.part_index + lt * A.part_count;
                     const int32_t px = (tile % A.tiles_x) * A.tile_w + it % A.tile_w;
                     const int32_t py = (tile / A.tiles_x) * A.tile_h + it / A.tile_w;
@@ -1261,6 +1277,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 o[1] = so.color.y;
                 o[2] = so.color.z;
                 if (STATS) st.c[ST_SAMPLES]++;
+                // deep paths (rare: trapped inside meshes, up to ~100x the mean cost) mark their
+                // slot for the next frame's work order
+                const int32_t bounces = A.max_depth - depth;
+                if (!STATS && A.slot_cost && bounces > 3) atomicAdd(&A.slot_cost[slot], (uint32_t)bounces);
                 ++sample;
                 if (sample >= sample_end) T.phase = PH_PIXEL;
                 else start_sample();
@@ -1309,6 +1329,17 @@ __global__ void accumulate_kernel(const float* __restrict__ colors, uint32_t n_s
         running[3 * (size_t)slot + 1] = sum.y;
         running[3 * (size_t)slot + 2] = sum.z;
     }
+}
+
+// per local tile: the summed slot costs (keys of the next frame's work order) and its index
+__global__ void tile_cost_kernel(const uint32_t* slot_cost, uint32_t n_tiles, uint32_t per_tile, uint32_t* tile_cost,
+                                 uint32_t* tile_index) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tiles) return;
+    uint32_t sum = 0;
+    for (uint32_t i = 0; i < per_tile; ++i) sum += slot_cost[(size_t)t * per_tile + i];
+    tile_cost[t] = sum;
+    tile_index[t] = t;
 }
 
 // scatter gathered tile buffers back into the image
@@ -1514,6 +1545,15 @@ struct rtw_gpu_world {
     int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
     int lds_cu = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerMultiprocessor
     TuneState* tune = nullptr;  // in-frame threshold tuning state
+    // work order (render_frame): per-slot costs accumulated over frames of one partition shape,
+    // and the tile order derived from them after each frame
+    uint32_t* slot_cost = nullptr;
+    uint32_t* tile_buf = nullptr;  // 4 x n_tiles: cost, index, sorted cost, permutation
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    uint64_t order_key[6] = {};    // total, part index / count, tiles_x, tile w / h of the costs
+    uint32_t order_tiles = 0;
+    bool order_valid = false;      // tile permutation computed for order_key
 };
 
 extern "C" RTW_API int rtw_device_count(int* count) {
@@ -1762,6 +1802,9 @@ extern "C" RTW_API int rtw_world_release(rtw_gpu_world* g) {
     if (g->queue) (void)hipFree(g->queue);
     if (g->colors) (void)hipFree(g->colors);
     if (g->tune) (void)hipFree(g->tune);
+    if (g->slot_cost) (void)hipFree(g->slot_cost);
+    if (g->tile_buf) (void)hipFree(g->tile_buf);
+    if (g->sort_tmp) (void)hipFree(g->sort_tmp);
     if (g->running) (void)hipFree(g->running);
     delete g;
     return RTW_OK;
@@ -1847,7 +1890,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     // items in flight blur epoch boundaries; mirrored candidates cancel the blur's bias); explore
     // only if warm-up + all epochs + one more fit (a 1080p x 512 spp frame split over 8 GPUs does)
     A.tune_items = 0;
-    if (A.tune && A.total > 0) {
+    if (A.tune && A.total > 0 && !A.tile_perm) {  // epochs are whole passes: chunk-major order only
         const uint64_t lanes = (uint64_t)blocks * RTW_BLOCK;
         const uint64_t E = (uint64_t)A.total * ((2 * lanes + A.total - 1) / A.total);
         if (A.items_big >= (uint64_t)(RTW_TUNE_EPOCHS + 2) * E) {
@@ -1873,11 +1916,13 @@ size_t env_size(const char* name, size_t dflt) {
 
 void set_items(KArgs& A, uint32_t chunk) {
     const uint32_t n = A.s_end - A.s_begin;
-    const uint32_t tail = std::min<uint32_t>(n, (uint32_t)env_size("RTW_TAIL_SAMPLES", 8));
+    // chunk-major order drains on single-sample items; in cost order the cheapest tiles come last
+    const uint32_t tail = A.tile_perm ? 0u : std::min<uint32_t>(n, (uint32_t)env_size("RTW_TAIL_SAMPLES", 8));
     A.chunk = chunk;
     A.s_split = A.s_end - tail;
     A.items_big = (uint64_t)A.total * ((A.s_split - A.s_begin + chunk - 1) / chunk);
     A.items = A.items_big + (uint64_t)A.total * tail;
+    A.chunks = (A.s_split - A.s_begin + chunk - 1) / chunk;
 }
 
 int grow(void** buf, size_t* have, size_t need) {
@@ -1917,6 +1962,42 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
     // fixes the threshold instead.
     A.tune = nullptr;
     if (!stats && !std::getenv("RTW_TRACE_MIN")) A.tune = g->tune;
+    // Work order.  A frame renders tiles in the order of the deep-path cost its slots showed in
+    // earlier frames of the same partition shape, costliest first, each tile's samples together:
+    // the frame then ends on cheap tiles instead of waiting for paths trapped inside a mesh that
+    // started late (about 100 ms per frame on suzanne).  The image does not depend on the order
+    // (a sample's RNG stream is keyed by pixel and sample; accumulation is in sample order).
+    // The first frame of a shape runs chunk-major (and hosts the threshold tuning).
+    // RTW_NO_REORDER=1 keeps chunk-major order.
+    A.slot_cost = nullptr;
+    A.tile_perm = nullptr;
+    const uint32_t per_tile = (uint32_t)(A.tile_w * A.tile_h);
+    const uint32_t n_tiles_local = A.total / per_tile;
+    const char* nr = std::getenv("RTW_NO_REORDER");
+    if (!stats && !(nr && nr[0] && nr[0] != '0')) {
+        const uint64_t key[6] = {A.total, (uint64_t)A.part_index, (uint64_t)A.part_count, (uint64_t)A.tiles_x,
+                                 (uint64_t)A.tile_w, (uint64_t)A.tile_h};
+        if (std::memcmp(key, g->order_key, sizeof(key)) != 0 || !g->slot_cost) {
+            if (g->slot_cost) (void)hipFree(g->slot_cost);
+            if (g->tile_buf) (void)hipFree(g->tile_buf);
+            if (g->sort_tmp) (void)hipFree(g->sort_tmp);
+            g->slot_cost = nullptr;
+            g->tile_buf = nullptr;
+            g->sort_tmp = nullptr;
+            g->order_valid = false;
+            HIP_TRY(hipMalloc(&g->slot_cost, (size_t)A.total * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&g->tile_buf, (size_t)n_tiles_local * 4 * sizeof(uint32_t)));
+            g->sort_tmp_bytes = 0;
+            HIP_TRY(rtw::sort_pairs_desc(nullptr, nullptr, nullptr, nullptr, (int)n_tiles_local, nullptr,
+                                         &g->sort_tmp_bytes, stream));
+            HIP_TRY(hipMalloc(&g->sort_tmp, std::max<size_t>(g->sort_tmp_bytes, 16)));
+            HIP_TRY(hipMemsetAsync(g->slot_cost, 0, (size_t)A.total * sizeof(uint32_t), stream));
+            std::memcpy(g->order_key, key, sizeof(key));
+            g->order_tiles = n_tiles_local;
+        }
+        A.slot_cost = g->slot_cost;
+        if (g->order_valid) A.tile_perm = g->tile_buf + 3 * (size_t)n_tiles_local;
+    }
     HIP_TRY(hipMemsetAsync(g->queue, 0, RTW_QUEUE_SLOTS * sizeof(unsigned long long), stream));
     int launch = 0;
     for (uint32_t s0 = 0; s0 < A.spp; s0 += (uint32_t)per_launch, ++launch) {
@@ -1933,6 +2014,16 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
                            A.total, g->running, s0 == 0 ? 1 : 0, s1 == A.spp ? 1 : 0, A.spp, out, A.layout, A.width,
                            A.height, A.tile_w, A.tile_h, A.tiles_x, A.part_index, A.part_count);
         HIP_TRY(hipGetLastError());
+    }
+    if (A.slot_cost && n_tiles_local > 0) {  // the next frame's tile order
+        uint32_t* tb = g->tile_buf;
+        const size_t n = n_tiles_local;
+        hipLaunchKernelGGL(tile_cost_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                           (const uint32_t*)g->slot_cost, (uint32_t)n, per_tile, tb, tb + n);
+        HIP_TRY(hipGetLastError());
+        size_t bytes = g->sort_tmp_bytes;
+        HIP_TRY(rtw::sort_pairs_desc(tb, tb + 2 * n, tb + n, tb + 3 * n, (int)n, g->sort_tmp, &bytes, stream));
+        g->order_valid = true;
     }
     return RTW_OK;
 }

@@ -139,3 +139,30 @@ def test_device_encoder_matches_host():
     encode_rgb8_device(d.data_ptr(), len(x) // 3, out.data_ptr(), 0)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), to_rgb8_gamma2(x.reshape(-1, 3)).ravel())
+
+
+@pytest.mark.parametrize("name,parts", [("suzanne", 1), ("suzanne", 3), ("final_scene1", 2)])
+def test_cost_ordered_frames_are_bit_identical(worlds, name, parts):
+    """Frames after the first of a partition shape run their tiles in measured-cost order
+    (render_frame's work order); every frame must equal the oracle bit for bit, whatever the order."""
+    import torch
+
+    from raytracinginaweekend_amd.distributed import FrameRenderer, FrameSpec, untile_host
+
+    world = worlds(name)
+    size = R.Size2i(72, 40)
+    spec = FrameSpec(size, 24, 50, 5)
+    ref = O.render(world, R.render_params(size, 24, 50, seed=5))
+    bufs = []
+    for rank in range(parts):
+        fr = FrameRenderer(world, spec, rank, parts, 0)
+        frames = []
+        for _ in range(3):  # chunk-major, then cost order twice
+            fr.launch()
+            torch.cuda.synchronize()
+            frames.append((fr.image if parts == 1 else fr.tiles).cpu().numpy().copy())
+        for f in frames[1:]:
+            assert_bit_identical(f, frames[0], f"{name} frame order rank {rank}")
+        bufs.append(frames[-1])
+    img = bufs[0].reshape(-1, 3) if parts == 1 else untile_host(np.concatenate(bufs), size, spec.tile, parts, len(bufs[0]))
+    assert_bit_identical(img, ref, name)
