@@ -80,15 +80,19 @@ struct WorldConst {
 // On-device tuning of the dynamic-fetch threshold, kept per world.  A launch that finds chosen == 0
 // and has room for it explores candidates over epochs of `tune_items` work items -- whole passes
 // over the launch's pixel slots, so every epoch renders the same pixels (other samples) and epoch
-// times compare like for like.  Epoch 0 warms up; epoch j = 1..EPOCHS runs candidate
-// cand[j-1] (mirrored, a..f f..a); the wave whose refill hands out the first item of an epoch
-// records the 100 MHz clock.  Once the last epoch has ended every wave derives the same winner
-// (least time over its two epochs) and publishes it for the world's later launches.
+// times compare like for like.  Epoch 0 warms up; epoch e = 1..EPOCHS runs candidate
+// cand[e-1] (mirrored, a..f f..a).  Only the second half of an epoch is timed: a switch of
+// threshold shifts how many lanes sit finished-but-unshaded, and that transient would bias the
+// first half (against low thresholds after high ones).  The wave whose refill hands out the first
+// item of a half-epoch records the 100 MHz clock.  Once the last epoch has ended every wave derives
+// the same winner (least timed half-epoch time over its two epochs) and publishes it for the
+// world's later launches.
 #define RTW_TUNE_NCAND 6
 #define RTW_TUNE_EPOCHS (2 * RTW_TUNE_NCAND)
+#define RTW_TUNE_STAMPS (2 * RTW_TUNE_EPOCHS + 2)
 struct TuneState {
-    unsigned long long tb[RTW_TUNE_EPOCHS + 1];  // clock when item (j + 1) * tune_items was handed out
-    int chosen;                                  // the world's threshold once decided (0: not yet)
+    unsigned long long tb[RTW_TUNE_STAMPS];  // clock when item (k + 1) * tune_items / 2 was handed out
+    int chosen;                              // the world's threshold once decided (0: not yet)
 };
 __constant__ const int kTuneCand[RTW_TUNE_NCAND] = {12, 16, 24, 32, 40, 48};
 
@@ -1131,10 +1135,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             unsigned long long base = 0;
             if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
             base = __shfl(base, leader);
-            if (!tuned) {  // wave-uniform; the batch holding an epoch's first item stamps its start
-                const uint64_t E = A.tune_items;
-                const uint64_t j = (base + E - 1) / E;
-                if (lane == leader && j >= 1 && j <= RTW_TUNE_EPOCHS + 1 && j * E < base + (uint64_t)__popcll(m))
+            if (!tuned) {  // wave-uniform; the batch holding a half-epoch's first item stamps its start
+                const uint64_t E = A.tune_items, H = E / 2;
+                const uint64_t j = (base + H - 1) / H;
+                if (lane == leader && j >= 1 && j <= RTW_TUNE_STAMPS && j * H < base + (uint64_t)__popcll(m))
                     __hip_atomic_store(&A.tune->tb[j - 1], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t e = base / E;
                 if (e == 0) {
@@ -1143,18 +1147,18 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     const int i = (int)e - 1;
                     trace_min = kTuneCand[i < RTW_TUNE_NCAND ? i : RTW_TUNE_EPOCHS - 1 - i];
                 } else {
-                    unsigned long long tb[RTW_TUNE_EPOCHS + 1];
+                    unsigned long long tb[RTW_TUNE_STAMPS];
                     bool ok = true;
-                    for (int k = 0; k <= RTW_TUNE_EPOCHS; ++k) {
+                    for (int k = 0; k < RTW_TUNE_STAMPS; ++k) {
                         tb[k] = __hip_atomic_load(&A.tune->tb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         ok = ok && tb[k] != ~0ull;
                     }
                     trace_min = A.trace_min;
-                    if (ok) {  // epoch j (1-based) lasted tb[j] - tb[j-1]
+                    if (ok) {  // epoch e's timed second half: items [(2e+1)H, (2e+2)H) = tb[2e+1] - tb[2e]
                         unsigned long long best_t = 0;
                         for (int c = 0; c < RTW_TUNE_NCAND; ++c) {
-                            const unsigned long long t = (tb[c + 1] - tb[c]) +
-                                                         (tb[RTW_TUNE_EPOCHS - c] - tb[RTW_TUNE_EPOCHS - 1 - c]);
+                            const int e1 = c + 1, e2 = RTW_TUNE_EPOCHS - c;
+                            const unsigned long long t = (tb[2 * e1 + 1] - tb[2 * e1]) + (tb[2 * e2 + 1] - tb[2 * e2]);
                             if (c == 0 || t < best_t) {
                                 best_t = t;
                                 trace_min = kTuneCand[c];
