@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out; rm -f gpurun_out/part8.txt
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit $?
+timeout -k 10 300 python tools/part_bench.py --scene suzanne --parts 4,8 --steps 2 >> gpurun_out/part8.txt 2>&1 || exit $?
+timeout -k 10 300 python tools/part_bench.py --scene final_scene1 --parts 8 --steps 2 >> gpurun_out/part8.txt 2>&1 || exit $?
