@@ -96,6 +96,27 @@ struct TuneState {
 };
 __constant__ const int kTuneCand[RTW_TUNE_NCAND] = {12, 16, 24, 32, 40, 48};
 
+// Division by a launch-invariant u32 (Granlund & Montgomery 1994, Thm 4.2, N = 32): with
+// s = ceil(log2 d) and m = floor(2^32 (2^s - d) / d) + 1, q = (mulhi(n, m) + n) >> s for every
+// n < 2^32 (the sum taken in 64 bits).  Replaces the work-item decode's integer divisions.
+struct FastDiv {
+    uint32_t d, m, s;
+};
+inline FastDiv fastdiv_make(uint32_t d) {
+    uint32_t s = 0;
+    while (s < 32 && (1ull << s) < d) ++s;
+    const uint64_t m = (((1ull << s) - d) << 32) / d + 1;
+    return FastDiv{d, (uint32_t)m, s};
+}
+__host__ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint32_t t = __umulhi(n, f.m);
+#else
+    const uint32_t t = (uint32_t)(((uint64_t)n * f.m) >> 32);
+#endif
+    return (uint32_t)(((uint64_t)t + n) >> f.s);
+}
+
 struct KArgs {
     DWorld w;
     int32_t width, height;
@@ -133,6 +154,8 @@ struct KArgs {
     const uint32_t* tile_perm;  // tile rank -> local tile, null: chunk-major order
     uint32_t* slot_cost;        // per slot: bounces of the deep (> 3 bounce) paths rendered there
     uint32_t chunks;            // chunks per slot in this launch (tile_perm order)
+    // work-item decode (items < 2^32 per launch, render_frame): divisors as FastDiv
+    FastDiv fd_total, fd_rank, fd_tile, fd_tiles_x, fd_tile_w;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -1082,7 +1105,6 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
     const int lane = threadIdx.x & 63;
-    const int per_tile = A.tile_w * A.tile_h;
 
     // Per-lane state machine.  Work items (a slot and a run of `chunk` consecutive samples) come
     // from a queue (wave-aggregated atomics), chunk-major so that a wave's lanes share a tile;
@@ -1177,26 +1199,25 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     T.phase = PH_TRACE;  // leaves the loops below
                 } else {
                     const bool big = item < A.items_big;
-                    const uint64_t rel = big ? item : item - A.items_big;
-                    uint32_t ck, c;
-                    int32_t lt, it;
+                    const uint32_t rel = (uint32_t)(big ? item : item - A.items_big);  // < 2^32
+                    uint32_t ck, c, lt, it;
                     if (A.tile_perm) {  // tile-major in cost order: tile rank, chunk, pixel of the tile
-                        const uint64_t per_rank = (uint64_t)per_tile * A.chunks;
-                        const uint32_t g = (uint32_t)(rel / per_rank);
-                        const uint32_t wi = (uint32_t)(rel - (uint64_t)g * per_rank);
-                        ck = wi / (uint32_t)per_tile;
-                        it = (int32_t)(wi - ck * (uint32_t)per_tile);
-                        lt = (int32_t)A.tile_perm[g];
-                        c = (uint32_t)lt * (uint32_t)per_tile + (uint32_t)it;
+                        const uint32_t g = fdiv(rel, A.fd_rank);
+                        const uint32_t wi = rel - g * A.fd_rank.d;
+                        ck = fdiv(wi, A.fd_tile);
+                        it = wi - ck * A.fd_tile.d;
+                        lt = A.tile_perm[g];
+                        c = lt * A.fd_tile.d + it;
                     } else {  // chunk-major: pass after pass over the slots
-                        ck = (uint32_t)(rel / A.total);
-                        c = (uint32_t)(rel - (uint64_t)ck * A.total);
-                        lt = (int32_t)(c / (uint32_t)per_tile);
-                        it = (int32_t)(c % (uint32_t)per_tile);
+                        ck = fdiv(rel, A.fd_total);
+                        c = rel - ck * A.total;
+                        lt = fdiv(c, A.fd_tile);
+                        it = c - lt * A.fd_tile.d;
                     }
-                    const int32_t tile = A.part_index + lt * A.part_count;
-                    const int32_t px = (tile % A.tiles_x) * A.tile_w + it % A.tile_w;
-                    const int32_t py = (tile / A.tiles_x) * A.tile_h + it / A.tile_w;
+                    const uint32_t tile = (uint32_t)A.part_index + lt * (uint32_t)A.part_count;
+                    const uint32_t ty = fdiv(tile, A.fd_tiles_x), iy = fdiv(it, A.fd_tile_w);
+                    const int32_t px = (int32_t)((tile - ty * (uint32_t)A.tiles_x) * (uint32_t)A.tile_w + (it - iy * (uint32_t)A.tile_w));
+                    const int32_t py = (int32_t)(ty * (uint32_t)A.tile_h + iy);
                     if (px < A.width && py < A.height) {  // else: padding slot of an edge tile
                         slot = c;
                         pix = (uint32_t)(py * A.width + px);
@@ -1927,6 +1948,12 @@ void set_items(KArgs& A, uint32_t chunk) {
     A.items_big = (uint64_t)A.total * ((A.s_split - A.s_begin + chunk - 1) / chunk);
     A.items = A.items_big + (uint64_t)A.total * tail;
     A.chunks = (A.s_split - A.s_begin + chunk - 1) / chunk;
+    const uint32_t per_tile = (uint32_t)(A.tile_w * A.tile_h);
+    A.fd_total = fastdiv_make(A.total);
+    A.fd_tile = fastdiv_make(per_tile);
+    A.fd_rank = fastdiv_make(per_tile * std::max<uint32_t>(1, A.chunks));
+    A.fd_tiles_x = fastdiv_make((uint32_t)A.tiles_x);
+    A.fd_tile_w = fastdiv_make((uint32_t)A.tile_w);
 }
 
 int grow(void** buf, size_t* have, size_t need) {
@@ -1953,6 +1980,9 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
     const size_t per_sample = (size_t)A.total * 3 * sizeof(float);
     uint64_t per_launch = std::max<uint64_t>(chunk, (budget / per_sample) / chunk * chunk);
     per_launch = std::min<uint64_t>(per_launch, A.spp);
+    // the kernel decodes work items in 32 bits: keep a launch's items (plus a wave's overrun of
+    // the queue) below 2^32
+    per_launch = std::min<uint64_t>(per_launch, std::max<uint64_t>(chunk, ((0xFFFFFFFFull >> 1) / A.total) / chunk * chunk));
     int rc = grow((void**)&g->colors, &g->colors_bytes, per_sample * per_launch);
     if (rc != RTW_OK) return rc;
     if (per_launch < A.spp) {
