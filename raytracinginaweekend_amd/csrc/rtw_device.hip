@@ -127,7 +127,7 @@ struct KArgs {
     int32_t tile_w, tile_h, tiles_x, n_tiles;
     int32_t part_index, part_count;
     uint32_t total;          // pixel slots in this partition (owned tiles * tile_w * tile_h)
-    int32_t node_count, leaf_count, tri_count;
+    int32_t node_count, leaf_count, rect_count, tri_count;
     unsigned long long* queue; // work-item counter (zeroed before each launch)
     // one launch renders samples [s_begin, s_end) of every slot as work items of `chunk`
     // consecutive samples (item = chunk index * total + slot); each finished sample's colour goes
@@ -965,17 +965,19 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
     }
 }
 
-// LDS modes of the render kernel: 0 scene in HBM, 1 nodes + leaf records + cull constants in LDS,
-// 2 also the plain-triangle records (tri_fast).  LDS layout: [node_a n][node_b n][leaf_fast L]
-// [km ceil(n/2)][tri_fast 4T (mode 2)][stack depth x BLOCK]
+// LDS modes of the render kernel: 0 scene in HBM, 1 nodes + leaf records + cull constants + rect
+// records in LDS, 2 also the plain-triangle records (tri_fast).  LDS layout: [node_a n][node_b n]
+// [leaf_fast L][km ceil(n/2)][rects 2R][tri_fast 4T (mode 2)][stack depth x BLOCK]
 template <bool STATS, int LDS>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
-                                      int32_t n_leaves, int32_t n_tris, unsigned long long* dbg) {
+                                      int32_t n_leaves, int32_t n_rects, int32_t n_tris, unsigned long long* dbg) {
     constexpr bool LDS_SCENE = LDS >= 1;
     const DWorld& w = *wp;
     // the plain-triangle records' base, loaded once per call into scalar registers (the world
     // struct is read through a pointer; left in the loop it becomes a dependent global load)
-    const int32_t tri_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
+    const int32_t rect_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
+    const int32_t tri_off = rect_off + 2 * n_rects;
+    const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
     const float4* tri_fast = LDS == 2 ? smem + tri_off : uniform_ptr(w.tri_fast);
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
     // The LDS section offsets are held in VGPRs (opaque copies): as SGPRs they compete with the
@@ -1025,6 +1027,17 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             if (sph.w == sph.w) {  // a plain sphere
                 if (STATS) st.c[ST_T_SPHERE]++;
                 sphere_leaf(sph, leaf, T.ray, T.te, T.found);
+            } else if (__float_as_int(sph.x) == 2) {  // a plain rect
+                if (STATS) st.c[ST_T_RECT]++;
+                const int ri = __float_as_int(sph.y);
+                const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
+                const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
+                float t;
+                V3 pos;
+                if (rect_t(g, T.ray, 0.001f, T.te, t, pos)) {
+                    T.te = t;
+                    T.found = leaf;
+                }
             } else if (__float_as_int(sph.x) == 1) {  // a plain triangle
                 if (STATS) st.c[ST_T_TRI]++;
                 float t;
@@ -1095,8 +1108,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
         float2* km = reinterpret_cast<float2*>(smem + 2 * A.node_count + A.leaf_count);
         for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = w.node_km[i];
+        float4* rects = smem + 2 * A.node_count + A.leaf_count + (A.node_count + 1) / 2;
+        for (int i = threadIdx.x; i < 2 * A.rect_count; i += RTW_BLOCK) rects[i] = w.rects[i];
         if (LDS == 2) {
-            float4* tris = smem + 2 * A.node_count + A.leaf_count + (A.node_count + 1) / 2;
+            float4* tris = rects + 2 * A.rect_count;
             for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[i] = w.tri_fast[i];
         }
         __syncthreads();
@@ -1254,7 +1269,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 
         // 3. traversal (hittable.rs:429-473)
         T = traverse<STATS, LDS>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, A.leaf_count,
-                                 A.tri_count,
+                                 A.rect_count, A.tri_count,
                                        STATS ? A.stats + ST_COUNT : nullptr);
         if (STATS) {
             c_mark = clock64();
@@ -1564,7 +1579,7 @@ struct rtw_gpu_world {
     DWorld w{};
     const DWorld* wdev = nullptr;
     int32_t node_count = 0, leaf_count = 0, depth = 1;
-    int32_t tri_count = 0;
+    int32_t tri_count = 0, rect_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int cus = 0;
     int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
@@ -1628,9 +1643,9 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
             const rtw_sphere& sp = w->spheres[l.geom_index];
             lf[(size_t)i] = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius);
         } else {
-            // w = NaN: not a plain sphere; x = 1 tags a plain triangle (index in y)
-            const bool tri = l.geom_kind == RTW_GEOM_TRIANGLE && l.flags == 0;
-            lf[(size_t)i] = make_float4(ibits(tri ? 1 : 0), ibits(l.geom_index), 0.0f, ibits(0x7FC00000));
+            // w = NaN: not a plain sphere; x = 1 tags a plain triangle, 2 a plain rect (index in y)
+            const int tag = l.flags != 0 ? 0 : (l.geom_kind == RTW_GEOM_TRIANGLE ? 1 : (l.geom_kind == RTW_GEOM_RECT ? 2 : 0));
+            lf[(size_t)i] = make_float4(ibits(tag), ibits(l.geom_index), 0.0f, ibits(0x7FC00000));
         }
     }
     const size_t o_lf = L.push(lf.data(), lf.size() * sizeof(float4));
@@ -1785,6 +1800,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->leaf_count = w->leaf_count;
     g->depth = std::max(1, depth);
     g->tri_count = w->triangle_count;
+    g->rect_count = w->rect_count;
     g->mk_world = 1;
     for (int i = 0; i < w->node_count; ++i)
         for (int k = 0; k < 3; ++k)
@@ -1870,6 +1886,7 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.leaf_count = g->leaf_count;
     A.mk_world = g->mk_world;
     A.tri_count = g->tri_count;
+    A.rect_count = g->rect_count;
     A.queue = g->queue;
     A.wdev = g->wdev;
     A.trace_min = 32;
@@ -1887,7 +1904,8 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
 enum LaunchKind { LK_RENDER, LK_STATS };
 int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const bool stats = kind == LK_STATS;
-    const size_t scene_bytes = (size_t)(2 * g->node_count + g->leaf_count + (g->node_count + 1) / 2) * sizeof(float4);
+    const size_t scene_bytes =
+        (size_t)(2 * g->node_count + g->leaf_count + (g->node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
     const size_t tri_bytes = (size_t)g->tri_count * 4 * sizeof(float4);
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
     // a block may take its share of the CU's LDS at the kernel's target occupancy
