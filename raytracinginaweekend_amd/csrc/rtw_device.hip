@@ -81,20 +81,20 @@ struct WorldConst {
 // and has room for it explores candidates over epochs of `tune_items` work items -- whole passes
 // over the launch's pixel slots, so every epoch renders the same pixels (other samples) and epoch
 // times compare like for like.  Epoch 0 warms up; epoch e = 1..EPOCHS runs candidate
-// cand[e-1] (mirrored, a..f f..a).  Only the second half of an epoch is timed: a switch of
+// cand[e-1] (mirrored, a..h h..a).  Only the second half of an epoch is timed: a switch of
 // threshold shifts how many lanes sit finished-but-unshaded, and that transient would bias the
 // first half (against low thresholds after high ones).  The wave whose refill hands out the first
 // item of a half-epoch records the 100 MHz clock.  Once the last epoch has ended every wave derives
 // the same winner (least timed half-epoch time over its two epochs) and publishes it for the
 // world's later launches.
-#define RTW_TUNE_NCAND 6
+#define RTW_TUNE_NCAND 8
 #define RTW_TUNE_EPOCHS (2 * RTW_TUNE_NCAND)
 #define RTW_TUNE_STAMPS (2 * RTW_TUNE_EPOCHS + 2)
 struct TuneState {
     unsigned long long tb[RTW_TUNE_STAMPS];  // clock when item (k + 1) * tune_items / 2 was handed out
     int chosen;                              // the world's threshold once decided (0: not yet)
 };
-__constant__ const int kTuneCand[RTW_TUNE_NCAND] = {12, 16, 24, 32, 40, 48};
+__constant__ const int kTuneCand[RTW_TUNE_NCAND] = {6, 8, 12, 16, 24, 32, 40, 48};
 
 // Division by a launch-invariant u32 (Granlund & Montgomery 1994, Thm 4.2, N = 32): with
 // s = ceil(log2 d) and m = floor(2^32 (2^s - d) / d) + 1, q = (mulhi(n, m) + n) >> s for every
