@@ -141,14 +141,17 @@ def test_device_encoder_matches_host():
     assert np.array_equal(out.cpu().numpy(), to_rgb8_gamma2(x.reshape(-1, 3)).ravel())
 
 
-@pytest.mark.parametrize("name,parts", [("suzanne", 1), ("suzanne", 3), ("final_scene1", 2)])
-def test_cost_ordered_frames_are_bit_identical(worlds, name, parts):
+@pytest.mark.parametrize("name,parts,buffer_bytes", [("suzanne", 1, 0), ("suzanne", 3, 0), ("final_scene1", 2, 0),
+                                                     ("final_scene1", 1, 72 * 40 * 12 * 8)])
+def test_cost_ordered_frames_are_bit_identical(worlds, name, parts, buffer_bytes, monkeypatch):
     """Frames after the first of a partition shape run their tiles in measured-cost order
     (render_frame's work order); every frame must equal the oracle bit for bit, whatever the order."""
     import torch
 
     from raytracinginaweekend_amd.distributed import FrameRenderer, FrameSpec, untile_host
 
+    if buffer_bytes:  # several launches per frame (8 samples each), each in cost order
+        monkeypatch.setenv("RTW_SAMPLE_BUFFER_BYTES", str(buffer_bytes))
     world = worlds(name)
     size = R.Size2i(72, 40)
     spec = FrameSpec(size, 24, 50, 5)
