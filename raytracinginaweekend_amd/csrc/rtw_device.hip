@@ -35,6 +35,12 @@
 #ifndef RTW_MIN_WAVES_PER_SIMD
 #define RTW_MIN_WAVES_PER_SIMD 4
 #endif
+#ifndef RTW_WAVE_BATCH
+#define RTW_WAVE_BATCH 64  // work items a wave reserves per global atomic (upper bound)
+#endif
+#ifndef RTW_BATCH_SPREAD
+#define RTW_BATCH_SPREAD 8  // a batch is at most 1/(SPREAD x waves) of the launch's remaining items
+#endif
 #define RTW_STACK 32    // per-lane traversal stack (LDS), >= the BVH depth (checked at upload)
 #ifndef RTW_LDS_SCENE_MAX
 #define RTW_LDS_SCENE_MAX (160 * 1024)  // LDS bytes per block the scene (+ stack) may take
@@ -1162,22 +1168,44 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         if (ch > 0) trace_min = ch;
         else tuned = A.tune_items == 0;
     }
+    // This wave's reserve of work items [w_next, w_end), taken from the launch's counter in batches
+    // (one global atomic per batch instead of per refill round: a single counter hit by every
+    // wave's refills throttled fast-sample worlds); batches shrink toward the end of the launch so
+    // that the last items still spread over all waves.
+    uint64_t w_next = 0, w_end = 0;
+    const uint64_t n_waves = (uint64_t)gridDim.x * (RTW_BLOCK / 64);
     for (;;) {
-        // 1. lanes without a pixel take the next ones (one atomic per wave per round)
+        // 1. lanes without a pixel take the next items of the wave's reserve
         bool out_of_work = false;
         for (;;) {
             const unsigned long long m = __ballot(T.phase == PH_PIXEL);
             if (m == 0) break;
             const int leader = __ffsll((long long)m) - 1;
-            unsigned long long base = 0;
-            if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
-            base = __shfl(base, leader);
-            if (!tuned) {  // wave-uniform; the batch holding a half-epoch's first item stamps its start
-                const uint64_t E = A.tune_items, H = E / 2;
-                const uint64_t j = (base + H - 1) / H;
-                if (lane == leader && j >= 1 && j <= RTW_TUNE_STAMPS && j * H < base + (uint64_t)__popcll(m))
-                    __hip_atomic_store(&A.tune->tb[j - 1], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t e = base / E;
+            const uint64_t need = (uint64_t)__popcll(m);
+            // the first `left` lanes take the reserve's rest, the others a new batch from `base`
+            const uint64_t left = min(need, w_end - w_next);
+            uint64_t base = w_end;
+            if (left < need) {
+                const uint64_t rest = A.items > w_end ? A.items - w_end : 0;
+                const uint64_t batch =
+                    max(need - left, min((uint64_t)RTW_WAVE_BATCH, rest / ((uint64_t)RTW_BATCH_SPREAD * n_waves)));
+                unsigned long long b = 0;
+                if (lane == leader) b = atomicAdd(A.queue, (unsigned long long)batch);
+                base = __shfl(b, leader);
+                if (!tuned) {  // wave-uniform; the batch holding a half-epoch's first item stamps its start
+                    const uint64_t H = A.tune_items / 2;
+                    const uint64_t j = (base + H - 1) / H;
+                    if (lane == leader && j >= 1 && j <= RTW_TUNE_STAMPS && j * H < base + batch)
+                        __hip_atomic_store(&A.tune->tb[j - 1], wall_clock64(), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+                w_end = base + batch;
+            }
+            const uint64_t first = w_next;
+            w_next = (left < need) ? base + (need - left) : w_next + need;
+            if (!tuned) {  // wave-uniform: the epoch of the items being handed out
+                const uint64_t E = A.tune_items;
+                const uint64_t e = w_next / E;
                 if (e == 0) {
                     trace_min = A.trace_min;
                 } else if (e <= RTW_TUNE_EPOCHS) {
@@ -1208,7 +1236,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             }
             if (T.phase == PH_PIXEL) {
                 const unsigned long long below = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
-                const uint64_t item = base + (uint64_t)__popcll(below);
+                const uint64_t r = (uint64_t)__popcll(below);
+                const uint64_t item = r < left ? first + r : base + (r - left);
                 if (item >= A.items) {
                     out_of_work = true;
                     T.phase = PH_TRACE;  // leaves the loops below
