@@ -38,6 +38,12 @@
 #ifndef RTW_WAVE_BATCH
 #define RTW_WAVE_BATCH 64  // work items a wave reserves per global atomic (upper bound)
 #endif
+#ifndef RTW_WAVE_BATCH_BIG
+#define RTW_WAVE_BATCH_BIG 256  // the same past the costly prefix of a cost-ordered launch
+#endif
+#ifndef RTW_BIG_BATCH_FROM
+#define RTW_BIG_BATCH_FROM 250  // that prefix, per mille of the launch's items (env overrides)
+#endif
 #ifndef RTW_BATCH_SPREAD
 #define RTW_BATCH_SPREAD 8  // a batch is at most 1/(SPREAD x waves) of the launch's remaining items
 #endif
@@ -160,6 +166,7 @@ struct KArgs {
     const uint32_t* tile_perm;  // tile rank -> local tile, null: chunk-major order
     uint32_t* slot_cost;        // per slot: bounces of the deep (> 3 bounce) paths rendered there
     uint32_t chunks;            // chunks per slot in this launch (tile_perm order)
+    uint64_t big_from;          // items from here on are reserved RTW_WAVE_BATCH_BIG at a time
     // work-item decode (items < 2^32 per launch, render_frame): divisors as FastDiv
     FastDiv fd_total, fd_rank, fd_tile, fd_tiles_x, fd_tile_w;
 };
@@ -1187,8 +1194,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             uint64_t base = w_end;
             if (left < need) {
                 const uint64_t rest = A.items > w_end ? A.items - w_end : 0;
-                const uint64_t batch =
-                    max(need - left, min((uint64_t)RTW_WAVE_BATCH, rest / ((uint64_t)RTW_BATCH_SPREAD * n_waves)));
+                // small batches while the costly tiles are handed out: a wave slowed by long paths
+                // must not sit on a large reserve of them (an 8-GPU suzanne rank: 2.4x at 256)
+                const uint64_t cap = w_end >= A.big_from ? RTW_WAVE_BATCH_BIG : RTW_WAVE_BATCH;
+                const uint64_t batch = max(need - left, min(cap, rest / ((uint64_t)RTW_BATCH_SPREAD * n_waves)));
                 unsigned long long b = 0;
                 if (lane == leader) b = atomicAdd(A.queue, (unsigned long long)batch);
                 base = __shfl(b, leader);
@@ -1995,6 +2004,9 @@ void set_items(KArgs& A, uint32_t chunk) {
     A.items_big = (uint64_t)A.total * ((A.s_split - A.s_begin + chunk - 1) / chunk);
     A.items = A.items_big + (uint64_t)A.total * tail;
     A.chunks = (A.s_split - A.s_begin + chunk - 1) / chunk;
+    // chunk-major launches keep small batches throughout; cost order after its costly prefix
+    A.big_from = A.tile_perm ? A.items / 1000 * std::min<size_t>(1000, env_size("RTW_BIG_BATCH_FROM", RTW_BIG_BATCH_FROM))
+                             : ~0ull;
     const uint32_t per_tile = (uint32_t)(A.tile_w * A.tile_h);
     A.fd_total = fastdiv_make(A.total);
     A.fd_tile = fastdiv_make(per_tile);
