@@ -7,14 +7,23 @@ all-gather + untile assembles the image on rank 0 (N > 1).  `value` = W*H*spp*st
 ranks wall time of the timed region (strong scaling: the frame is fixed, N GPUs share it).
 
 Extra fields:
-  roofline      the render kernel's algorithmic bytes per launch (SURVEY §8(d) byte model, from
-                the kernel's counting variant over this rank's partition) / its average launch
-                time measured with HIP events on the launch stream; peak = 8 TB/s HBM3E.
-  cpu_baseline  the C restatement of the reference render loop (oracle/) on this host's cores,
-                N = 1 only, on a bounded sample of the same frame: every P-th 8x8 tile at the
-                full spp (P set for ~15 s of CPU work).
+  roofline      the render kernel against its real bound, VALU instruction issue: wave-level VALU
+                instructions of one timed frame (rocprofv3 --pmc SQ_INSTS_VALU pass of this same
+                benchmark) / the frame's render-launch time measured live with HIP events on the
+                launch stream, against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+                instruction (MI355X_MICROARCH.md).  Also: VALU lane utilisation, effective clock,
+                the SURVEY §8(d) algorithmic-bytes rate (`effective_GBps`: node / primitive
+                records served from LDS and L2, not HBM) and the measured HBM `traffic`.
+  cpu_baseline  the C restatement of the reference render loop (oracle/) in the reference's own
+                scheme (ref mode: per-thread xoroshiro streams, split_work_tasks + merge_planes,
+                rendering.rs:121-252) on all of this host's CPUs (nproc), N = 1 only: the
+                configured frame at a reduced spp (render time is linear in spp), plus config C1
+                (400x225x64) in full.
+  first_frame_ms  one cold drop-in rtw_render of the configured frame (upload, tuning frame in
+                chunk-major order, copy back): what a single reference-style render call costs.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (--gpus N > 1 without torchrun: starts N rank processes itself, before any GPU call)
        torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -29,6 +38,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CLOCK_GHZ = 2.4        # MI355X peak engine clock (MI355X_MICROARCH.md)
+SIMDS_PER_CU = 4       # SIMD-32 units per CU; a wave64 VALU instruction issues over 2 cycles
+VALU_COUNTERS = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVE_CYCLES",
+                 "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE")
 
 
 def alg_bytes(stats: dict, pixels: int) -> int:
@@ -46,12 +59,11 @@ def alg_bytes(stats: dict, pixels: int) -> int:
     )
 
 
-def pmc_traffic(args) -> dict | None:
-    """HBM bytes of one render-kernel launch from rocprofv3 PMC counters (MI355X_MICROARCH.md
-    HBM section): a child `rocprofv3 --pmc FETCH_SIZE` run and a separate `--pmc WRITE_SIZE` run
-    of this same benchmark (1 frame, no warmup), each reading the frame's render_kernel dispatch.
-    FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 reports half the bytes of wide coalesced reads in
-    FETCH_SIZE, so it is doubled.  None if rocprofv3 is unavailable or a pass fails."""
+def _pmc_pass(args, counters) -> dict | None:
+    """One `rocprofv3 --pmc <counters>` run of this benchmark (1 warm-up + 1 timed frame, no extra
+    legs): per counter, the sum over the timed frame's render_kernel dispatches (the last half of
+    them; counters of one dispatch may come as several rows), plus that frame's dispatch time
+    from the trace timestamps.  None if rocprofv3 is unavailable or the pass fails."""
     import csv
     import glob
     import shutil
@@ -62,70 +74,159 @@ def pmc_traffic(args) -> dict | None:
         return None
     child = [sys.executable, os.path.abspath(__file__), "--scene", args.scene, "--width", str(args.width), "--height",
              str(args.height), "--spp", str(args.spp), "--max-depth", str(args.max_depth), "--seed", str(args.seed),
-             "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-stats", "--no-traffic"]
-    got = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
-            cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "pmc", "--output-format", "csv", "--"] + child
-            try:
-                subprocess.run(cmd, check=True, capture_output=True, timeout=600, cwd=ROOT)
-            except (subprocess.SubprocessError, OSError):
-                return None
-            rows = []
-            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-                rows += [r for r in csv.DictReader(open(f)) if "render_kernel" in r["Kernel_Name"]
-                         and r["Counter_Name"] == counter]
-            if not rows:
-                return None
-            # the child renders one frame: sum its render launches (one per <= 16 GiB of
-            # per-sample colours; counters of one dispatch may come as several rows)
-            got[counter] = sum(float(r["Counter_Value"]) for r in rows) * 1024.0
-            got["launches"] = len({r["Dispatch_Id"] for r in rows})
-    fetch = got["FETCH_SIZE"] * 2.0
-    return {"fetch_bytes": fetch, "write_bytes": got["WRITE_SIZE"], "bytes": fetch + got["WRITE_SIZE"],
-            "launches": got["launches"]}
+             "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-stats", "--no-pmc", "--no-first-frame"]
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+        cmd = ["rocprofv3", "--pmc", *counters, "-d", d, "-o", "pmc", "--output-format", "csv", "--"] + child
+        try:
+            subprocess.run(cmd, check=True, capture_output=True, timeout=600, cwd=ROOT)
+        except (subprocess.SubprocessError, OSError):
+            return None
+        rows = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            rows += [r for r in csv.DictReader(open(f)) if "render_kernel" in r["Kernel_Name"]]
+    if not rows:
+        return None
+    ids = sorted({int(r["Dispatch_Id"]) for r in rows})
+    timed = set(ids[len(ids) // 2:])  # two frames with the same launch count: the second is timed
+    got: dict = {"launches": len(timed)}
+    span = {}
+    for r in rows:
+        if int(r["Dispatch_Id"]) not in timed:
+            continue
+        got[r["Counter_Name"]] = got.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        span[r["Dispatch_Id"]] = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+    got["dispatch_ns"] = sum(e - s for s, e in span.values())
+    return got
 
 
-def cpu_baseline(world, args) -> dict:
-    """The reference algorithm on the host cores (oracle/, test infrastructure), on a bounded
-    sample of the same frame: every P-th 8x8 tile (interleaved, like the GPU partition) at the
-    full spp, P chosen so the sample takes about --cpu-seconds."""
+def pmc_traffic(args) -> dict | None:
+    """HBM bytes of the timed frame's render launches (MI355X_MICROARCH.md HBM section): separate
+    FETCH_SIZE and WRITE_SIZE passes; both count KiB, and gfx950 reports half the bytes of wide
+    coalesced reads in FETCH_SIZE, so it is doubled."""
+    f = _pmc_pass(args, ["FETCH_SIZE"])
+    w = _pmc_pass(args, ["WRITE_SIZE"]) if f else None
+    if not f or not w or "FETCH_SIZE" not in f or "WRITE_SIZE" not in w:
+        return None
+    fetch = f["FETCH_SIZE"] * 1024.0 * 2.0
+    write = w["WRITE_SIZE"] * 1024.0
+    return {"fetch_bytes": fetch, "write_bytes": write, "bytes": fetch + write, "launches": f["launches"]}
+
+
+def pmc_valu(args) -> dict | None:
+    """VALU issue counters of the timed frame (one pass: 6 SQ + 1 GRBM counters)."""
+    c = _pmc_pass(args, list(VALU_COUNTERS))
+    if not c or any(k not in c for k in VALU_COUNTERS):
+        return None
+    return c
+
+
+def _cpu_info() -> dict:
+    """nproc, the CPUs this process may run on, the cgroup CPU quota and the CPU model."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = info["nproc"]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_quota_cpus"] = None
+    info["model"] = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return info
+
+
+def cpu_baseline(args) -> dict:
+    """The reference algorithm in its own RNG/thread scheme (oracle ref mode, test infrastructure)
+    on every CPU this process may use: the configured frame at a reduced spp (whole image, the
+    reference's sample split over `threads` planes; time is linear in spp), and config C1
+    (final_scene1 400x225x64, max_depth 50) in full."""
     import numpy as np
 
     import raytracinginaweekend_amd as R
     from oracle import pyoracle as O
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    size = R.Size2i(args.width, args.height)
-    out = np.zeros((size.count(), 3), np.float32)
-    n_tiles = -(-args.width // 8) * -(-args.height // 8)
+    info = _cpu_info()
+    usable = info["affinity"]
+    if info["cgroup_quota_cpus"]:  # more threads than the quota only time-slice the same CPU time
+        usable = min(usable, max(1, int(info["cgroup_quota_cpus"] + 0.5)))
+    threads = args.cpu_threads or min(512, usable)
 
-    def run(parts, spp):
-        p = R.render_params(size, spp, args.max_depth, seed=3, part=(0, parts))
+    def run(world, w, h, spp):
+        out = np.zeros((w * h, 3), np.float32)
+        p = R.render_params(R.Size2i(w, h), spp, args.max_depth, seed=3)
         t = time.perf_counter()
-        O.render(world, p, O.RNG_CTR, threads, out=out)
-        dt = time.perf_counter() - t
-        return len(range(0, n_tiles, parts)) * 64 * spp, dt
+        O.render(world, p, O.RNG_REF, threads, out=out)
+        return time.perf_counter() - t
 
-    n, dt = run(48, 16)  # calibration, ~1 s
-    for _ in range(3):
-        rate = n / dt
-        parts = max(1, min(n_tiles, int(args.width * args.height * args.spp / (rate * args.cpu_seconds))))
-        n, dt = run(parts, args.spp)
-        if dt > 0.5 * args.cpu_seconds or parts == 1:
-            break
+    c1_dt = run(R.demo_world("final_scene1"), 400, 225, 64)  # C1 in full; also calibrates the spp below
+    c1_rate = 400 * 225 * 64 / c1_dt
+    spp = int(args.cpu_seconds * c1_rate / (args.width * args.height))
+    spp = max(min(threads, args.spp), min(args.spp, max(1, spp)))  # every thread gets a plane
+    dt = run(R.demo_world(args.scene), args.width, args.height, spp)
+    rate = args.width * args.height * spp / dt / 1e6
     return {
-        "value": round(n / dt / 1e6, 4),
+        "value": round(rate, 4),
         "unit": "Msamples/sec",
         "cores": threads,
+        "cores_note": "threads = the CPUs this process can use (affinity, capped by the cgroup CPU quota)",
         "kind": "port",
-        "sample": f"{args.scene} {args.width}x{args.height} at {args.spp}spp, every {parts}th 8x8 tile "
-        f"({n} samples), max_depth {args.max_depth}; C restatement of rendering.rs (oracle/), "
-        f"{threads} threads over rows, {dt:.1f} s",
+        "sample": f"{args.scene} {args.width}x{args.height} at {spp} spp (of {args.spp}; time is linear in spp), "
+        f"max_depth {args.max_depth}, {dt:.1f} s; the reference's scheme (oracle ref mode: per-thread xoroshiro "
+        f"streams, split_work_tasks over {threads} threads, merge_planes)",
+        "nproc": info["nproc"],
+        "affinity_cpus": info["affinity"],
+        "cgroup_quota_cpus": info["cgroup_quota_cpus"],
+        "cpu_model": info["model"],
+        "c1": {"workload": "final_scene1 400x225x64spp max_depth 50 (BASELINE configs[0]), full frame",
+               "seconds": round(c1_dt, 3), "Msamples_per_s": round(400 * 225 * 64 / c1_dt / 1e6, 4)},
     }
 
 
-def main() -> None:
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: one rank process per GPU, started before this process
+    touches the GPU (counting devices does not initialise it); rank 0 prints the line."""
+    import socket
+    import subprocess
+
+    import torch
+
+    n = torch.cuda.device_count()
+    if n < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {n}", file=sys.stderr)
+        return 3
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # a failed rank leaves the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -138,17 +239,25 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
-    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes (VALU counters, HBM traffic)")
+    ap.add_argument("--no-traffic", action="store_true", help="skip only the HBM traffic passes")
+    ap.add_argument("--no-first-frame", action="store_true")
     ap.add_argument("--stats-spp", type=int, default=128, help="spp of the counting render (scaled to --spp)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--save", default="", help="write the rank-0 image (.ppm/.png)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args)
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_size != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world_size} ranks", file=sys.stderr)
+        return 2
+
     import torch  # first: librtw.so then binds to the same libamdhip64.so.7 instance
 
     rank = int(os.environ.get("RANK", "0"))
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -156,6 +265,7 @@ def main() -> None:
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == world_size
 
     import raytracinginaweekend_amd as R
     from raytracinginaweekend_amd.distributed import FrameRenderer, FrameSpec
@@ -174,12 +284,13 @@ def main() -> None:
         fr.render_frame()
     barrier()
 
+    # HIP events on the stream the render kernel is launched on (the current stream)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
         starts[i].record()
-        fr.launch()  # the render kernel, on the current stream
+        fr.launch()  # the render kernel (+ the in-order accumulation), on the current stream
         ends[i].record()
         fr.exchange()
     barrier()
@@ -193,8 +304,22 @@ def main() -> None:
 
     samples = args.width * args.height * args.spp * args.steps
     value = samples / elapsed / 1e6
+    pix = fr.pixels_this_rank()
 
-    roofline = None
+    first_frame_ms = None
+    if rank == 0 and world_size == 1 and not args.no_first_frame:
+        t = time.perf_counter()
+        R.render(spec.size, 1, args.spp, args.max_depth, world, seed=args.seed, device=local_rank)
+        first_frame_ms = round((time.perf_counter() - t) * 1e3, 1)
+
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    peak_ginstr = cus * SIMDS_PER_CU * CLOCK_GHZ / 2.0  # G wave-level VALU instructions / s
+    roofline = {"bound": "valu_issue", "achieved": None, "peak": round(peak_ginstr, 1), "unit": "G VALU wave-instr/s",
+                "frac": None, "traffic": None,
+                "kernel": "render_kernel<false, LDS mode>; HIP events on its launch stream also span the in-order "
+                          "accumulate_kernel (~0.3 % of the frame)",
+                "kernel_ms": round(kernel_ms, 3),
+                "peak_basis": f"{cus} CUs x {SIMDS_PER_CU} SIMD-32 x {CLOCK_GHZ} GHz / 2 cycles per wave64 VALU instruction"}
     if not args.no_stats:
         # the counting variant is ~8x slower than the product kernel: count at a bounded spp and
         # scale to the frame's (per-sample counts do not depend on spp; samples are independent)
@@ -203,37 +328,48 @@ def main() -> None:
         stats = fr.dworld.collect_stats(sp)
         scale = args.spp / sp.samples_per_pixel
         stats = {k: int(round(v * scale)) for k, v in stats.items()}
-        pix = fr.pixels_this_rank()
         b = alg_bytes(stats, pix)
-        achieved = b / (kernel_ms * 1e-3) / 1e9
-        roofline = {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "kernel": "render_kernel<false, LDS mode> (HIP events also span the in-order accumulate_kernel)",
-            "counts": f"counting variant at {min(args.spp, args.stats_spp)} spp, scaled x{args.spp / min(args.spp, args.stats_spp):g}",
-            "kernel_ms": round(kernel_ms, 3),
-            "alg_bytes_per_launch": b,
-            "per_sample": {k: round(v / max(1, stats["samples"]), 3) for k, v in stats.items() if k != "samples"},
-        }
+        roofline["effective_GBps"] = round(b / (kernel_ms * 1e-3) / 1e9, 1)
+        roofline["effective_note"] = ("SURVEY §8(d) algorithmic record bytes / kernel time: node and primitive records "
+                                      "come from LDS and L2, so this is not HBM bandwidth (see traffic)")
+        roofline["alg_bytes_per_launch"] = b
+        roofline["counts"] = f"counting variant at {sp.samples_per_pixel} spp, scaled x{scale:g}"
+        roofline["per_sample"] = {k: round(v / max(1, stats["samples"]), 3) for k, v in stats.items() if k != "samples"}
+
+    if rank == 0 and world_size == 1 and not args.no_pmc:
+        v = pmc_valu(args)
+        if v is not None:
+            insts = v["SQ_INSTS_VALU"]
+            achieved = insts / (kernel_ms * 1e-3) / 1e9
+            dispatch_s = v["dispatch_ns"] * 1e-9
+            roofline["achieved"] = round(achieved, 1)
+            roofline["frac"] = round(achieved / peak_ginstr, 4)
+            roofline["valu"] = {
+                "insts_per_frame": int(insts),
+                "lane_utilisation": round(v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"]), 4),
+                "wait_any_frac": round(v["SQ_WAIT_ANY"] / v["SQ_WAVE_CYCLES"], 4),
+                "effective_clock_GHz": round(v["GRBM_GUI_ACTIVE"] / 8.0 / dispatch_s / 1e9, 3) if dispatch_s > 0 else None,
+                "pmc_dispatch_ms": round(dispatch_s * 1e3, 3),
+                "source": "rocprofv3 --pmc " + " ".join(VALU_COUNTERS) + f" on this benchmark's timed frame "
+                          f"({v['launches']} render launch(es)); lane utilisation = SQ_THREAD_CYCLES_VALU / "
+                          "(64 x SQ_ACTIVE_INST_VALU); clock = GRBM_GUI_ACTIVE / 8 XCDs / dispatch time",
+            }
+        if not args.no_traffic:
+            t = pmc_traffic(args)
+            if t is not None:
+                roofline["traffic"] = round(t["bytes"])
+                roofline["hbm_GBps"] = round(t["bytes"] / (kernel_ms * 1e-3) / 1e9, 1)
+                roofline["hbm_frac"] = round(t["bytes"] / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                roofline["traffic_detail"] = {
+                    "fetch_bytes_x2": round(t["fetch_bytes"]), "write_bytes": round(t["write_bytes"]),
+                    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), the timed frame's "
+                              f"render_kernel launches ({t['launches']})"}
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(world, args)
-    if roofline is not None and rank == 0 and world_size == 1 and not args.no_traffic:
-        t = pmc_traffic(args)
-        if t is not None:
-            roofline["traffic"] = round(t["bytes"])
-            roofline["traffic_detail"] = {"fetch_bytes_x2": round(t["fetch_bytes"]), "write_bytes": round(t["write_bytes"]),
-                                          "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one frame's render_kernel "
-                                                    f"launches ({t['launches']})"}
+        cpu = cpu_baseline(args)
 
     if args.save and rank == 0:
-        import numpy as np
-
         from raytracinginaweekend_amd.image_io import save_image
 
         torch.cuda.synchronize(dev)
@@ -261,8 +397,10 @@ def main() -> None:
                 "spp": args.spp,
                 "max_depth": args.max_depth,
                 "partition": f"interleaved {spec.tile[0]}x{spec.tile[1]} tiles over {world_size} GPU(s)",
+                "rccl_world_size": world_size,
                 "trace_min": fr.dworld.tuned_trace_min(),
             },
+            "first_frame_ms": first_frame_ms,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -270,7 +408,8 @@ def main() -> None:
 
     if world_size > 1:
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

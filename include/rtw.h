@@ -35,7 +35,7 @@ extern "C" {
 #endif
 
 #define RTW_API __attribute__((visibility("default")))
-#define RTW_ABI_VERSION 1
+#define RTW_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define RTW_OK 0
@@ -214,6 +214,14 @@ typedef struct rtw_render_params {
     int32_t tile_height;        /* 0 -> 8 */
     int32_t part_index;         /* this caller renders tiles t with t % part_count == part_index */
     int32_t part_count;         /* 0 -> 1 */
+    /* thread_count of rendering::render (rendering.rs:121-128): the reference splits the samples
+     * into thread_count planes (split_work_tasks, rendering.rs:222-237: the first spp % T planes
+     * take one sample more, planes of 0 samples are dropped), averages each plane over its own
+     * sample count and merges them last-plane-first (merge_planes, rendering.rs:239-252).  The
+     * device reproduces that arithmetic exactly (plane t sums samples start_t.. in order).
+     * 0 -> 1 (one plane: sum / spp). */
+    int32_t thread_count;
+    int32_t reserved0; /* must be 0 */
 } rtw_render_params;
 
 /* Traversal statistics of one render (for the algorithmic-bytes model). */

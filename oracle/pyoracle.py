@@ -55,6 +55,9 @@ def lib():
         L.rtw_oracle_ray_color.restype = C.c_int
         L.rtw_oracle_ray_color.argtypes = [C.POINTER(N.World), C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_float,
                                            C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_float)]
+        L.rtw_oracle_sample_color.restype = C.c_int
+        L.rtw_oracle_sample_color.argtypes = [C.POINTER(N.World), C.POINTER(N.RenderParams), C.c_int32, C.c_int32,
+                                              C.c_uint32, C.POINTER(C.c_float)]
         L.rtw_oracle_eval_scalar.restype = C.c_int
         L.rtw_oracle_eval_scalar.argtypes = [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int64,
                                              C.POINTER(C.c_float)]
@@ -76,6 +79,15 @@ def render(world, params: N.RenderParams, rng_mode: int = RNG_CTR, threads: int 
     if rc != 0:
         raise RuntimeError(f"oracle render failed: {rc}")
     return (out, st.as_dict()) if stats else out
+
+
+def sample_color(world, params: N.RenderParams, x: int, y: int, s: int) -> np.ndarray:
+    """The ctr-mode radiance of sample `s` of pixel (x, y) (one term of the per-pixel sum)."""
+    out = np.zeros(3, np.float32)
+    rc = lib().rtw_oracle_sample_color(world.ptr(), C.byref(params), x, y, s, out.ctypes.data_as(C.POINTER(C.c_float)))
+    if rc != 0:
+        raise RuntimeError("oracle sample_color failed")
+    return out
 
 
 def scene_hit(world, origin, direction, time=0.0, t_start=0.001, t_end=float("inf"), rng=(1, 2)):

@@ -787,27 +787,43 @@ static void* ctr_worker(void* arg) {
     c.rng = &rng;
     c.st = j->want_stats ? &j->st : NULL;
     c.km = j->km;
+    const uint32_t T = p->thread_count > 1 ? (uint32_t)p->thread_count : 1u;
+    const uint32_t whole = p->samples_per_pixel / T, rem = p->samples_per_pixel % T;
+    const uint32_t n_planes = whole > 0 ? T : rem;
+    V3* plane = (V3*)malloc(sizeof(V3) * n_planes);
     for (int y = j->row_begin; y < H; y += j->row_step) {
         for (int x = 0; x < W; ++x) {
             if (!tile_owned(p, x, y)) continue;
             const uint32_t pix = (uint32_t)(y * W + x);
             const float fx = (float)x * sx, fy = (float)y * sy;
-            V3 sum = v3(0.0f, 0.0f, 0.0f);
-            for (uint32_t s = 0; s < p->samples_per_pixel; ++s) {
-                rng = rtw_sample_stream(key, pix, s);
-                const float jx = rtw_uniform_sample(&ux, &rng);
-                const float jy = rtw_uniform_sample(&uy, &rng);
-                const Ray r = camera_ray(&j->w->camera, &rng, fx + jx, fy + jy);
-                sum = vadd(sum, mode_ray_color(&c, &r, p->max_depth, p->render_mode));
-                if (c.st) c.st->samples++;
+            /* thread_count planes (split_work_tasks, rendering.rs:222-237), each the in-order sum
+             * of its sample range / its count (rendering.rs:172-179); with ctr streams plane t
+             * renders the global samples start_t .. start_t + n_t - 1 */
+            uint32_t s = 0;
+            for (uint32_t t = 0; t < n_planes; ++t) {
+                const uint32_t n_t = whole + (t < rem ? 1u : 0u);
+                V3 sum = v3(0.0f, 0.0f, 0.0f);
+                for (uint32_t k = 0; k < n_t; ++k, ++s) {
+                    rng = rtw_sample_stream(key, pix, s);
+                    const float jx = rtw_uniform_sample(&ux, &rng);
+                    const float jy = rtw_uniform_sample(&uy, &rng);
+                    const Ray r = camera_ray(&j->w->camera, &rng, fx + jx, fy + jy);
+                    sum = vadd(sum, mode_ray_color(&c, &r, p->max_depth, p->render_mode));
+                    if (c.st) c.st->samples++;
+                }
+                plane[t] = vdiv(sum, (float)n_t);
             }
-            const V3 px = vdiv(sum, (float)p->samples_per_pixel);
+            /* merge_planes (rendering.rs:239-252): last plane, += planes 0..n-2, * (1/n) */
+            V3 px = plane[n_planes - 1];
+            for (uint32_t t = 0; t + 1 < n_planes; ++t) px = vadd(px, plane[t]);
+            if (n_planes > 1) px = vmul(px, 1.0f / (float)n_planes);
             float* o = j->out + (size_t)pix * 3u;
             o[0] = px.e[0];
             o[1] = px.e[1];
             o[2] = px.e[2];
         }
     }
+    free(plane);
     return NULL;
 }
 
@@ -1006,6 +1022,27 @@ RTW_API int rtw_oracle_ray_color(const rtw_world* w, const float origin[3], cons
     for (int i = 0; i < 3; ++i) color[i] = col.e[i];
     rng_state[0] = rng.s0;
     rng_state[1] = rng.s1;
+    return RTW_OK;
+}
+
+/* One camera sample's radiance in ctr mode: pixel (x, y), global sample index s (the per-sample
+ * term of rendering.rs:172-178 before any summation). */
+RTW_API int rtw_oracle_sample_color(const rtw_world* w, const rtw_render_params* p, int32_t x, int32_t y, uint32_t s,
+                                    float color[3]) {
+    const int v = validate(w, p);
+    if (v != RTW_OK) return v;
+    const int W = p->width, H = p->height;
+    if (x < 0 || y < 0 || x >= W || y >= H) return RTW_ERR_INVALID_ARGUMENT;
+    const rtw_uniform ux = rtw_uniform_new(0.0f, 1.0f / (float)(W - 1));
+    const rtw_uniform uy = rtw_uniform_new(0.0f, 1.0f / (float)(H - 1));
+    rtw_xoro rng = rtw_sample_stream(rtw_seed_key(p->seed), (uint32_t)(y * W + x), s);
+    Ctx c = {w, &rng, NULL, NULL};
+    const float jx = rtw_uniform_sample(&ux, &rng);
+    const float jy = rtw_uniform_sample(&uy, &rng);
+    const Ray r = camera_ray(&w->camera, &rng, (float)x * (1.0f / (float)(W - 1)) + jx,
+                             (float)y * (1.0f / (float)(H - 1)) + jy);
+    const V3 col = mode_ray_color(&c, &r, p->max_depth, p->render_mode);
+    for (int i = 0; i < 3; ++i) color[i] = col.e[i];
     return RTW_OK;
 }
 

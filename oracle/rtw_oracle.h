@@ -56,6 +56,10 @@ RTW_API int rtw_oracle_ray_color(const rtw_world* w, const float origin[3], cons
                                  float time, int32_t max_depth, int32_t mode, uint64_t rng[2],
                                  float color[3]);
 
+/* One ctr-mode camera sample's radiance: pixel (x, y), global sample index s. */
+RTW_API int rtw_oracle_sample_color(const rtw_world* w, const rtw_render_params* p, int32_t x, int32_t y,
+                                    uint32_t s, float color[3]);
+
 /* Scalar spec evaluation on the host (for the device self-test comparison). */
 RTW_API int rtw_oracle_eval_scalar(int fn, const float* a, const float* b, int64_t n, float* out);
 

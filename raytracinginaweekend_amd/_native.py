@@ -161,6 +161,8 @@ class RenderParams(C.Structure):
         ("tile_height", C.c_int32),
         ("part_index", C.c_int32),
         ("part_count", C.c_int32),
+        ("thread_count", C.c_int32),
+        ("reserved0", C.c_int32),
     ]
 
 
@@ -228,6 +230,7 @@ class RtwError(RuntimeError):
         self.code = code
 
 
+ABI_VERSION = 2  # RTW_ABI_VERSION of include/rtw.h
 _lib = None
 
 _P = C.c_void_p
@@ -309,6 +312,8 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if not os.environ.get("RTW_LIBRARY") and L.rtw_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} has ABI version {L.rtw_version()}, this package needs {ABI_VERSION}: rebuild it")
         _lib = L
     return _lib
 

@@ -138,6 +138,7 @@ struct KArgs {
     int32_t layout;
     int32_t tile_w, tile_h, tiles_x, n_tiles;
     int32_t part_index, part_count;
+    int32_t thread_count;    // the reference's sample-split planes (accumulation only)
     uint32_t total;          // pixel slots in this partition (owned tiles * tile_w * tile_h)
     int32_t node_count, leaf_count, rect_count, tri_count;
     unsigned long long* queue; // work-item counter (zeroed before each launch)
@@ -1409,14 +1410,70 @@ __global__ void accumulate_kernel(const float* __restrict__ colors, uint32_t n_s
     }
 }
 
-// per local tile: the summed slot costs (keys of the next frame's work order) and its index
-__global__ void tile_cost_kernel(const uint32_t* slot_cost, uint32_t n_tiles, uint32_t per_tile, uint32_t* tile_cost,
+// The reference's thread_count > 1 (rendering.rs:161-219): split_work_tasks gives plane t the
+// samples [start_t, start_t + n_t) with n_t = whole + (t < rem) (planes of 0 samples dropped), each
+// plane is its samples' in-order sum / n_t (rendering.rs:172-179), and merge_planes adds the last
+// plane first, then planes 0..n-2 in order, then multiplies by 1/n (rendering.rs:239-252).  Per slot:
+// `planes` holds the n plane partials / values between launches (plane-major, 3 floats per slot);
+// this launch's samples [s0, s1) are added to the planes they belong to, a plane that ends here is
+// divided by its count, and the frame's last launch merges.
+__global__ void accumulate_planes_kernel(const float* __restrict__ colors, uint32_t s0, uint32_t s1, uint32_t total,
+                                         float* __restrict__ planes, uint32_t n_planes, uint32_t whole, uint32_t rem,
+                                         int last, float* out, int layout, int32_t width, int32_t height,
+                                         int32_t tile_w, int32_t tile_h, int32_t tiles_x, int32_t part_index,
+                                         int32_t part_count) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= total) return;
+    const int32_t per_tile = tile_w * tile_h;
+    const int32_t tile = part_index + (int32_t)(slot / (uint32_t)per_tile) * part_count;
+    const int32_t it = (int32_t)(slot % (uint32_t)per_tile);
+    const int32_t px = (tile % tiles_x) * tile_w + it % tile_w;
+    const int32_t py = (tile / tiles_x) * tile_h + it / tile_w;
+    if (px >= width || py >= height) return;  // padding slot of an edge tile
+    const size_t pstride = 3 * (size_t)total;
+    for (uint32_t t = 0; t < n_planes; ++t) {
+        const uint32_t n_t = whole + (t < rem ? 1u : 0u);
+        const uint32_t a = t * whole + min(t, rem), b = a + n_t;
+        if (b <= s0 || a >= s1) continue;
+        float* P = planes + t * pstride + 3 * (size_t)slot;
+        V3 sum = a < s0 ? v3(P[0], P[1], P[2]) : v3(0.0f, 0.0f, 0.0f);
+        const uint32_t lo = max(a, s0), hi = min(b, s1);
+        const float* c = colors + ((size_t)(lo - s0) * total + slot) * 3;
+        for (uint32_t s = lo; s < hi; ++s, c += pstride) sum = add(sum, v3(c[0], c[1], c[2]));
+        if (b <= s1) sum = divs(sum, (float)n_t);  // .sum::<Color>() / real_samples_per_pixel as f32
+        P[0] = sum.x;
+        P[1] = sum.y;
+        P[2] = sum.z;
+    }
+    if (!last) return;
+    const float* L = planes + (n_planes - 1) * pstride + 3 * (size_t)slot;
+    V3 r = v3(L[0], L[1], L[2]);  // planes.pop()
+    for (uint32_t t = 0; t + 1 < n_planes; ++t) {
+        const float* P = planes + t * pstride + 3 * (size_t)slot;
+        r = add(r, v3(P[0], P[1], P[2]));
+    }
+    r = mul(r, 1.0f / (float)n_planes);  // multiplier = 1.0 / planes.len() as f32
+    float* o = (layout == RTW_LAYOUT_TILES) ? out + 3 * (size_t)slot : out + 3 * ((size_t)py * width + px);
+    o[0] = r.x;
+    o[1] = r.y;
+    o[2] = r.z;
+}
+
+// per local tile: the summed slot costs (keys of the next frame's work order, saturated to 32 bits)
+// and its index; the slot costs then decay by half, so the order follows the recent frames (a
+// changed seed or camera re-weights within a few frames) and the per-slot counters stay bounded
+// (<= 2x one frame's deep bounces: 50 x 2048 spp x 2 < 2^18 per slot)
+__global__ void tile_cost_kernel(uint32_t* slot_cost, uint32_t n_tiles, uint32_t per_tile, uint32_t* tile_cost,
                                  uint32_t* tile_index) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
-    uint32_t sum = 0;
-    for (uint32_t i = 0; i < per_tile; ++i) sum += slot_cost[(size_t)t * per_tile + i];
-    tile_cost[t] = sum;
+    uint64_t sum = 0;
+    for (uint32_t i = 0; i < per_tile; ++i) {
+        const uint32_t c = slot_cost[(size_t)t * per_tile + i];
+        sum += c;
+        slot_cost[(size_t)t * per_tile + i] = c >> 1;
+    }
+    tile_cost[t] = (uint32_t)min<uint64_t>(sum, 0xFFFFFFFFull);
     tile_index[t] = t;
 }
 
@@ -1629,7 +1686,9 @@ struct rtw_gpu_world {
     uint32_t* tile_buf = nullptr;  // 4 x n_tiles: cost, index, sorted cost, permutation
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
-    uint64_t order_key[6] = {};    // total, part index / count, tiles_x, tile w / h of the costs
+    uint64_t order_key[10] = {};   // partition shape + workload (seed, spp, max_depth, mode) of the costs
+    hipEvent_t done = nullptr;     // end of the last frame rendered with this world's buffers
+    bool done_recorded = false;
     uint32_t order_tiles = 0;
     bool order_valid = false;      // tile permutation computed for order_key
 };
@@ -1885,6 +1944,7 @@ extern "C" RTW_API int rtw_world_release(rtw_gpu_world* g) {
     if (g->tile_buf) (void)hipFree(g->tile_buf);
     if (g->sort_tmp) (void)hipFree(g->sort_tmp);
     if (g->running) (void)hipFree(g->running);
+    if (g->done) (void)hipEventDestroy(g->done);
     delete g;
     return RTW_OK;
 }
@@ -1902,7 +1962,10 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     const int th = p->tile_height > 0 ? p->tile_height : 8;
     const int pc = p->part_count > 0 ? p->part_count : 1;
     if (p->part_index < 0 || p->part_index >= pc) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "part_index out of range");
+    if (p->thread_count < 0) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "thread_count must be >= 0");
+    if (p->reserved0 != 0) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "reserved0 must be 0");
     std::memset(&A, 0, sizeof(A));
+    A.thread_count = std::max(1, p->thread_count);
     A.w = g->w;
     A.width = p->width;
     A.height = p->height;
@@ -2031,10 +2094,25 @@ int grow(void** buf, size_t* have, size_t need) {
 // Launch l of a frame takes its work items from counter min(l, RTW_QUEUE_SLOTS - 1) of the
 // world's queue block, so a progress poller can read how many items each launch has handed out.
 #define RTW_QUEUE_SLOTS 32
+int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream,
+                      std::vector<uint64_t>* launch_items);
+
+// One render at a time per world: a frame reuses the world's queue, colour, running-sum and
+// cost buffers, so a frame issued on another stream first waits for the previous frame's end.
 int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream,
                  std::vector<uint64_t>* launch_items = nullptr) {
+    if (!g->done) HIP_TRY(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
+    if (g->done_recorded) HIP_TRY(hipStreamWaitEvent(stream, g->done, 0));
+    const int rc = render_frame_body(g, A, stats, out, stream, launch_items);
+    HIP_TRY(hipEventRecord(g->done, stream));
+    g->done_recorded = true;
+    return rc;
+}
+
+int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream,
+                      std::vector<uint64_t>* launch_items) {
     if (A.total == 0) return RTW_OK;
-    const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 8));
+    const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 1));
     const size_t budget = env_size("RTW_SAMPLE_BUFFER_BYTES", (size_t)16 << 30);
     const size_t per_sample = (size_t)A.total * 3 * sizeof(float);
     uint64_t per_launch = std::max<uint64_t>(chunk, (budget / per_sample) / chunk * chunk);
@@ -2044,7 +2122,14 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
     per_launch = std::min<uint64_t>(per_launch, std::max<uint64_t>(chunk, ((0xFFFFFFFFull >> 1) / A.total) / chunk * chunk));
     int rc = grow((void**)&g->colors, &g->colors_bytes, per_sample * per_launch);
     if (rc != RTW_OK) return rc;
-    if (per_launch < A.spp) {
+    // split_work_tasks (rendering.rs:222-237): planes of spp / T samples, the first spp % T one more
+    const uint32_t T = (uint32_t)std::max(1, A.thread_count);
+    const uint32_t whole = A.spp / T, rem = A.spp % T;
+    const uint32_t n_planes = whole > 0 ? T : rem;
+    if (n_planes > 1) {
+        rc = grow((void**)&g->running, &g->running_bytes, per_sample * n_planes);
+        if (rc != RTW_OK) return rc;
+    } else if (per_launch < A.spp) {
         rc = grow((void**)&g->running, &g->running_bytes, per_sample);
         if (rc != RTW_OK) return rc;
     }
@@ -2068,8 +2153,9 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
     const uint32_t n_tiles_local = A.total / per_tile;
     const char* nr = std::getenv("RTW_NO_REORDER");
     if (!stats && !(nr && nr[0] && nr[0] != '0')) {
-        const uint64_t key[6] = {A.total, (uint64_t)A.part_index, (uint64_t)A.part_count, (uint64_t)A.tiles_x,
-                                 (uint64_t)A.tile_w, (uint64_t)A.tile_h};
+        const uint64_t key[10] = {A.total, (uint64_t)A.part_index, (uint64_t)A.part_count, (uint64_t)A.tiles_x,
+                                  (uint64_t)A.tile_w, (uint64_t)A.tile_h, A.seed_key, A.spp, (uint64_t)(uint32_t)A.max_depth,
+                                  (uint64_t)(uint32_t)A.mode};
         if (std::memcmp(key, g->order_key, sizeof(key)) != 0 || !g->slot_cost) {
             if (g->slot_cost) (void)hipFree(g->slot_cost);
             if (g->tile_buf) (void)hipFree(g->tile_buf);
@@ -2103,16 +2189,21 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
         rc = launch_render(g, A, stats ? LK_STATS : LK_RENDER, stream);
         if (rc != RTW_OK) return rc;
         const unsigned blocks = (A.total + 255) / 256;
-        hipLaunchKernelGGL(accumulate_kernel, dim3(blocks), dim3(256), 0, stream, (const float*)g->colors, s1 - s0,
-                           A.total, g->running, s0 == 0 ? 1 : 0, s1 == A.spp ? 1 : 0, A.spp, out, A.layout, A.width,
-                           A.height, A.tile_w, A.tile_h, A.tiles_x, A.part_index, A.part_count);
+        if (n_planes > 1)
+            hipLaunchKernelGGL(accumulate_planes_kernel, dim3(blocks), dim3(256), 0, stream, (const float*)g->colors, s0,
+                               s1, A.total, g->running, n_planes, whole, rem, s1 == A.spp ? 1 : 0, out, A.layout,
+                               A.width, A.height, A.tile_w, A.tile_h, A.tiles_x, A.part_index, A.part_count);
+        else
+            hipLaunchKernelGGL(accumulate_kernel, dim3(blocks), dim3(256), 0, stream, (const float*)g->colors, s1 - s0,
+                               A.total, g->running, s0 == 0 ? 1 : 0, s1 == A.spp ? 1 : 0, A.spp, out, A.layout,
+                               A.width, A.height, A.tile_w, A.tile_h, A.tiles_x, A.part_index, A.part_count);
         HIP_TRY(hipGetLastError());
     }
     if (A.slot_cost && n_tiles_local > 0) {  // the next frame's tile order
         uint32_t* tb = g->tile_buf;
         const size_t n = n_tiles_local;
-        hipLaunchKernelGGL(tile_cost_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                           (const uint32_t*)g->slot_cost, (uint32_t)n, per_tile, tb, tb + n);
+        hipLaunchKernelGGL(tile_cost_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, g->slot_cost,
+                           (uint32_t)n, per_tile, tb, tb + n);
         HIP_TRY(hipGetLastError());
         size_t bytes = g->sort_tmp_bytes;
         HIP_TRY(rtw::sort_pairs_desc(tb, tb + 2 * n, tb + n, tb + 3 * n, (int)n, g->sort_tmp, &bytes, stream));

@@ -29,6 +29,7 @@ class FrameSpec:
     max_depth: int
     seed: int = 0x5EED
     tile: tuple[int, int] = (8, 8)
+    thread_count: int = 1  # the reference's sample-split planes (rendering.rs:222-252)
 
 
 def tile_slots(size: Size2i, tile: tuple[int, int], part: tuple[int, int]) -> np.ndarray:
@@ -76,7 +77,8 @@ class TileExchange:
         self.stride = partition_floats(p0)  # rank 0 owns the most tiles
         self.params = render_params(spec.size, spec.samples_per_pixel, spec.max_depth, seed=spec.seed,
                                     tile=spec.tile, part=(rank, world_size),
-                                    layout=N.LAYOUT_TILES if world_size > 1 else N.LAYOUT_IMAGE)
+                                    layout=N.LAYOUT_TILES if world_size > 1 else N.LAYOUT_IMAGE,
+                                    thread_count=spec.thread_count)
 
     def pixels_this_rank(self) -> int:
         return int((tile_slots(self.spec.size, self.spec.tile, (self.rank, self.world_size)) >= 0).sum())

@@ -1,9 +1,11 @@
 """rendering::render on the MI355X (src/lib/rendering.rs:121-252).
 
-`render` keeps the reference signature.  `thread_count` is accepted for signature parity and
-ignored: the device path has no sample split, every pixel sums all of its samples in order
-(equivalent to the reference with thread_count = 1, where merge_planes multiplies by 1.0).
-The reference seeds from entropy (rendering.rs:160); here the seed is explicit.
+`render` keeps the reference signature.  `thread_count` keeps its meaning for the numbers: the
+reference splits each pixel's samples into thread_count planes (split_work_tasks,
+rendering.rs:222-237), averages each plane over its own sample count and merges the planes
+last-first (merge_planes, rendering.rs:239-252); the device accumulation reproduces exactly that
+arithmetic (the parallelism itself is the GPU's, not thread_count threads).  The reference seeds
+from entropy (rendering.rs:160); here the seed is explicit.
 """
 from __future__ import annotations
 
@@ -47,8 +49,12 @@ def render_params(
     tile: tuple[int, int] = (8, 8),
     part: tuple[int, int] = (0, 1),
     layout: int = N.LAYOUT_IMAGE,
+    thread_count: int = 1,
 ) -> N.RenderParams:
+    if thread_count < 1:  # split_work_tasks divides by thread_count (rendering.rs:223): the reference panics
+        raise ValueError("thread_count must be >= 1")
     p = N.RenderParams()
+    p.thread_count = thread_count
     p.width, p.height = image_size.width, image_size.height
     p.samples_per_pixel = samples_per_pixel
     p.max_depth = max_depth
@@ -77,8 +83,7 @@ def render(
     progress: optional callable(done_samples, total_samples), called about every 50 ms while the
     frame renders and once at the end -- the reference's progress thread (rendering.rs:140-157)
     reports the same quantity as a percentage on stderr."""
-    del thread_count
-    p = render_params(image_size, samples_per_pixel, max_depth, render_mode, seed)
+    p = render_params(image_size, samples_per_pixel, max_depth, render_mode, seed, thread_count=thread_count)
     out = np.zeros((image_size.height * image_size.width, 3), np.float32)
     ptr = out.ctypes.data_as(C.POINTER(C.c_float))
     if progress is None:

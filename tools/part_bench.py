@@ -2,7 +2,7 @@
 (launch only, no gather) and which dynamic-fetch threshold it tunes.  Estimates the driver's
 N-GPU bench (aggregate ~ N x the slowest rank's rate) without N GPUs.
 
-python tools/part_bench.py [--scene final_scene1] [--parts 1,2,4,8] [--ranks 0,last] [--steps 3]
+python tools/part_bench.py [--scene final_scene1] [--parts 1,2,4,8] [--ranks ends|all] [--steps 3]
 """
 import argparse
 import os
@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--parts", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--max-depth", type=int, default=50)
+    ap.add_argument("--ranks", default="ends", help="'ends' (0 and N-1) or 'all'")
     a = ap.parse_args()
     import torch
 
@@ -30,7 +31,7 @@ def main():
     world = R.demo_world(a.scene)
     spec = FrameSpec(R.Size2i(a.width, a.height), a.spp, a.max_depth, 0x5EED)
     for n in [int(x) for x in a.parts.split(",")]:
-        for rank in sorted({0, n - 1}):
+        for rank in (range(n) if a.ranks == "all" else sorted({0, n - 1})):
             fr = FrameRenderer(world, spec, rank, n, 0)
             fr.launch()  # warm-up frame (tunes the threshold when the frame has room)
             torch.cuda.synchronize()
