@@ -982,7 +982,12 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 // LDS modes of the render kernel: 0 scene in HBM, 1 nodes + leaf records + cull constants + rect
 // records in LDS, 2 also the plain-triangle records (tri_fast).  LDS layout: [node_a n][node_b n]
 // [leaf_fast L][km ceil(n/2)][rects 2R][tri_fast 4T (mode 2)][stack depth x BLOCK]
-template <bool STATS, int LDS>
+// Leaf kinds of the world (LK): 0 plain spheres only, 1 plain spheres / rects / triangles,
+// 2 any (wrapped leaves, boxes, volumes: the generic leaf path).  A world without generic leaves
+// gets a loop without that path: the generic path's rng update alone made the compiler copy the
+// lane's traversal registers at the leaf merge on every leaf step.
+enum { LK_SPHERES = 0, LK_PLAIN = 1, LK_ANY = 2 };
+template <bool STATS, int LDS, int LK>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
                                       int32_t n_leaves, int32_t n_rects, int32_t n_tris, unsigned long long* dbg) {
     constexpr bool LDS_SCENE = LDS >= 1;
@@ -1038,7 +1043,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         if (T.phase == PH_TRACE && T.node < 0) {
             const int leaf = -1 - T.node;
             const float4 sph = fast[leaf];
-            if (sph.w == sph.w) {  // a plain sphere
+            if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
                 if (STATS) st.c[ST_T_SPHERE]++;
                 sphere_leaf(sph, leaf, T.ray, T.te, T.found);
             } else if (__float_as_int(sph.x) == 2) {  // a plain rect
@@ -1052,14 +1057,14 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                     T.te = t;
                     T.found = leaf;
                 }
-            } else if (__float_as_int(sph.x) == 1) {  // a plain triangle
+            } else if (LK == LK_PLAIN || __float_as_int(sph.x) == 1) {  // a plain triangle
                 if (STATS) st.c[ST_T_TRI]++;
                 float t;
                 if (tri_test(load_tri(tri_fast, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) {
                     T.te = t;
                     T.found = leaf;
                 }
-            } else {
+            } else if (LK == LK_ANY) {
                 float t;
                 if (leaf_t<STATS>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) {
                     T.te = t;
@@ -1108,7 +1113,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     return T;
 }
 
-template <bool STATS, int LDS>
+template <bool STATS, int LDS, int LK>
 __device__ __forceinline__ void render_body(const KArgs& A) {
     constexpr bool LDS_SCENE = LDS >= 1;
     // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
@@ -1307,7 +1312,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
 
         // 3. traversal (hittable.rs:429-473)
-        T = traverse<STATS, LDS>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, A.leaf_count,
+        T = traverse<STATS, LDS, LK>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, A.leaf_count,
                                  A.rect_count, A.tri_count,
                                        STATS ? A.stats + ST_COUNT : nullptr);
         if (STATS) {
@@ -1374,9 +1379,9 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     }
 }
 
-template <bool STATS, int LDS>
+template <bool STATS, int LDS, int LK>
 __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
-    render_body<STATS, LDS>(A);
+    render_body<STATS, LDS, LK>(A);
 }
 // Per slot: sum += colour of each sample of this launch, in sample order (the running sum of
 // earlier launches is carried in `running`); the last launch writes sum / spp (rendering.rs:179;
@@ -1676,6 +1681,7 @@ struct rtw_gpu_world {
     int32_t node_count = 0, leaf_count = 0, depth = 1;
     int32_t tri_count = 0, rect_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
+    int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
     int cus = 0;
     int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
     int lds_cu = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerMultiprocessor
@@ -1899,6 +1905,12 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->tri_count = w->triangle_count;
     g->rect_count = w->rect_count;
     g->mk_world = 1;
+    g->leaf_kinds = LK_SPHERES;
+    for (int i = 0; i < w->leaf_count; ++i) {
+        const rtw_leaf& l = w->leaves[i];
+        if (l.flags != 0 || l.geom_kind == RTW_GEOM_BOX) g->leaf_kinds = LK_ANY;
+        else if (l.geom_kind != RTW_GEOM_SPHERE && g->leaf_kinds == LK_SPHERES) g->leaf_kinds = LK_PLAIN;
+    }
     for (int i = 0; i < w->node_count; ++i)
         for (int k = 0; k < 3; ++k)
             for (float c : {w->nodes[i].min[k], w->nodes[i].max[k]})
@@ -2019,9 +2031,16 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     if (const char* e = std::getenv("RTW_LDS_MODE")) mode = std::min(mode, std::atoi(e));  // audits: cap the mode
     const size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes : 0) + stack_bytes;
     using KFn = void (*)(KArgs);
-    static const KFn fns[2][3] = {{render_kernel<false, 0>, render_kernel<false, 1>, render_kernel<false, 2>},
-                                  {render_kernel<true, 0>, render_kernel<true, 1>, render_kernel<true, 2>}};
-    const KFn kf = fns[stats ? 1 : 0][mode];
+    static const KFn fns[3][3] = {
+        {render_kernel<false, 0, LK_SPHERES>, render_kernel<false, 1, LK_SPHERES>, render_kernel<false, 2, LK_SPHERES>},
+        {render_kernel<false, 0, LK_PLAIN>, render_kernel<false, 1, LK_PLAIN>, render_kernel<false, 2, LK_PLAIN>},
+        {render_kernel<false, 0, LK_ANY>, render_kernel<false, 1, LK_ANY>, render_kernel<false, 2, LK_ANY>}};
+    static const KFn fns_stats[3] = {render_kernel<true, 0, LK_ANY>, render_kernel<true, 1, LK_ANY>,
+                                     render_kernel<true, 2, LK_ANY>};
+    // the leaf kinds the world needs; RTW_LEAF_KINDS=2 forces the generic loop (audits)
+    int lk = g->leaf_kinds;
+    if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(2, std::atoi(e)));
+    const KFn kf = stats ? fns_stats[mode] : fns[lk][mode];
     const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;
