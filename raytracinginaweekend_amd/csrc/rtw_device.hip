@@ -710,12 +710,15 @@ __device__ __forceinline__ float marble_k(const float* ranvec, const uint32_t* p
     return 1.0f + d_sinf(pz * scale + 10.0f * turb);
 }
 
-template <bool STATS>
+// TX: the world's textures are all SolidColor (TX_SOLID) or not (TX_ANY: checker, marble, image)
+enum { TX_SOLID = 0, TX_ANY = 1 };
+template <bool STATS, int TX>
 __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit& h, Stats& st) {  // texture.rs:23-53
     for (int guard = 0; guard < 64; ++guard) {
         const int4 t0 = w.textures[3 * tex];
         const int kind = t0.x;
-        if (kind == RTW_TEX_SOLID) return v3(__int_as_float(t0.y), __int_as_float(t0.z), __int_as_float(t0.w));
+        if (TX == TX_SOLID || kind == RTW_TEX_SOLID)
+            return v3(__int_as_float(t0.y), __int_as_float(t0.z), __int_as_float(t0.w));
         const int4 t1 = w.textures[3 * tex + 1];
         if (kind == RTW_TEX_CHECKER) {
             const float f = __int_as_float(t1.x);
@@ -820,7 +823,7 @@ struct ShadeOut {
     uint32_t texels;
 };
 
-template <bool STATS>
+template <bool STATS, int TX>
 __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t mode, Path P, int32_t found, float te,
                                        V3 pdir) {
     const DWorld& w = *wp;
@@ -912,7 +915,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                         sdir = sv;
                     }
                 }
-                const V3 tc = (tex >= 0) ? texture_sample<STATS>(w, tex, h, st) : v3(0.0f, 0.0f, 0.0f);
+                const V3 tc = (tex >= 0) ? texture_sample<STATS, TX>(w, tex, h, st) : v3(0.0f, 0.0f, 0.0f);
                 const V3 emitted = (mkind == RTW_MAT_DIFFUSE_LIGHT) ? tc : v3(0.0f, 0.0f, 0.0f);
                 const V3 albedo = (mkind == RTW_MAT_DIELECTRIC) ? v3(1.0f, 1.0f, 1.0f) : tc;
                 if (scatters) {
@@ -1113,7 +1116,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     return T;
 }
 
-template <bool STATS, int LDS, int LK>
+template <bool STATS, int LDS, int LK, int TX>
 __device__ __forceinline__ void render_body(const KArgs& A) {
     constexpr bool LDS_SCENE = LDS >= 1;
     // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
@@ -1227,23 +1230,30 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     const int i = (int)e - 1;
                     trace_min = kTuneCand[i < RTW_TUNE_NCAND ? i : RTW_TUNE_EPOCHS - 1 - i];
                 } else {
-                    unsigned long long tb[RTW_TUNE_STAMPS];
-                    bool ok = true;
-                    for (int k = 0; k < RTW_TUNE_STAMPS; ++k) {
-                        tb[k] = __hip_atomic_load(&A.tune->tb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok = ok && tb[k] != ~0ull;
+                    // epoch e's timed second half: items [(2e+1)H, (2e+2)H) = tb[2e+1] - tb[2e].  Four
+                    // stamps at a time (an array of all 34 stamps was the kernel's register peak)
+                    const unsigned long long* tbp = A.tune->tb;
+                    auto stamp = [&](int k) {
+                        return __hip_atomic_load(&tbp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    };
+                    bool ok = stamp(0) != ~0ull && stamp(1) != ~0ull;
+                    unsigned long long best_t = 0;
+                    int best = A.trace_min;
+#pragma nounroll
+                    for (int c = 0; c < RTW_TUNE_NCAND; ++c) {
+                        const int e1 = c + 1, e2 = RTW_TUNE_EPOCHS - c;
+                        const unsigned long long a0 = stamp(2 * e1), a1 = stamp(2 * e1 + 1), b0 = stamp(2 * e2),
+                                                 b1 = stamp(2 * e2 + 1);
+                        ok = ok && a0 != ~0ull && a1 != ~0ull && b0 != ~0ull && b1 != ~0ull;
+                        const unsigned long long t = (a1 - a0) + (b1 - b0);
+                        if (c == 0 || t < best_t) {
+                            best_t = t;
+                            best = kTuneCand[c];
+                        }
                     }
                     trace_min = A.trace_min;
-                    if (ok) {  // epoch e's timed second half: items [(2e+1)H, (2e+2)H) = tb[2e+1] - tb[2e]
-                        unsigned long long best_t = 0;
-                        for (int c = 0; c < RTW_TUNE_NCAND; ++c) {
-                            const int e1 = c + 1, e2 = RTW_TUNE_EPOCHS - c;
-                            const unsigned long long t = (tb[2 * e1 + 1] - tb[2 * e1]) + (tb[2 * e2 + 1] - tb[2 * e2]);
-                            if (c == 0 || t < best_t) {
-                                best_t = t;
-                                trace_min = kTuneCand[c];
-                            }
-                        }
+                    if (ok) {
+                        trace_min = best;
                         if (lane == leader) atomicCAS(&A.tune->chosen, 0, trace_min);
                         tuned = true;
                     }
@@ -1347,7 +1357,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             P.acc = acc;
             P.depth = depth;
             P.rng = T.rng;
-            const ShadeOut so = shade<STATS>(A.wdev, A.mode, P, T.found, T.te, pdir);
+            const ShadeOut so = shade<STATS, TX>(A.wdev, A.mode, P, T.found, T.te, pdir);
             T.ray = so.p.ray;
             att = so.p.att;
             acc = so.p.acc;
@@ -1379,9 +1389,9 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     }
 }
 
-template <bool STATS, int LDS, int LK>
+template <bool STATS, int LDS, int LK, int TX>
 __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
-    render_body<STATS, LDS, LK>(A);
+    render_body<STATS, LDS, LK, TX>(A);
 }
 // Per slot: sum += colour of each sample of this launch, in sample order (the running sum of
 // earlier launches is carried in `running`); the last launch writes sum / spp (rendering.rs:179;
@@ -1682,6 +1692,7 @@ struct rtw_gpu_world {
     int32_t tri_count = 0, rect_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
+    int32_t tex_kinds = TX_ANY;   // TX_*: the texture code the world's textures need
     int cus = 0;
     int lds_max = 64 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock
     int lds_cu = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerMultiprocessor
@@ -1906,6 +1917,9 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->rect_count = w->rect_count;
     g->mk_world = 1;
     g->leaf_kinds = LK_SPHERES;
+    g->tex_kinds = TX_SOLID;
+    for (int i = 0; i < w->texture_count; ++i)
+        if (w->textures[i].kind != RTW_TEX_SOLID) g->tex_kinds = TX_ANY;
     for (int i = 0; i < w->leaf_count; ++i) {
         const rtw_leaf& l = w->leaves[i];
         if (l.flags != 0 || l.geom_kind == RTW_GEOM_BOX) g->leaf_kinds = LK_ANY;
@@ -2031,16 +2045,18 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     if (const char* e = std::getenv("RTW_LDS_MODE")) mode = std::min(mode, std::atoi(e));  // audits: cap the mode
     const size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes : 0) + stack_bytes;
     using KFn = void (*)(KArgs);
-    static const KFn fns[3][3] = {
-        {render_kernel<false, 0, LK_SPHERES>, render_kernel<false, 1, LK_SPHERES>, render_kernel<false, 2, LK_SPHERES>},
-        {render_kernel<false, 0, LK_PLAIN>, render_kernel<false, 1, LK_PLAIN>, render_kernel<false, 2, LK_PLAIN>},
-        {render_kernel<false, 0, LK_ANY>, render_kernel<false, 1, LK_ANY>, render_kernel<false, 2, LK_ANY>}};
-    static const KFn fns_stats[3] = {render_kernel<true, 0, LK_ANY>, render_kernel<true, 1, LK_ANY>,
-                                     render_kernel<true, 2, LK_ANY>};
-    // the leaf kinds the world needs; RTW_LEAF_KINDS=2 forces the generic loop (audits)
-    int lk = g->leaf_kinds;
+#define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}
+    static const KFn fns[2][3][3] = {{RTW_KSET(LK_SPHERES, TX_SOLID), RTW_KSET(LK_PLAIN, TX_SOLID), RTW_KSET(LK_ANY, TX_SOLID)},
+                                     {RTW_KSET(LK_SPHERES, TX_ANY), RTW_KSET(LK_PLAIN, TX_ANY), RTW_KSET(LK_ANY, TX_ANY)}};
+#undef RTW_KSET
+    static const KFn fns_stats[3] = {render_kernel<true, 0, LK_ANY, TX_ANY>, render_kernel<true, 1, LK_ANY, TX_ANY>,
+                                     render_kernel<true, 2, LK_ANY, TX_ANY>};
+    // the leaf and texture kinds the world needs; RTW_LEAF_KINDS=2 / RTW_TEX_KINDS=1 force the
+    // generic code (audits)
+    int lk = g->leaf_kinds, tx = g->tex_kinds;
     if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(2, std::atoi(e)));
-    const KFn kf = stats ? fns_stats[mode] : fns[lk][mode];
+    if (const char* e = std::getenv("RTW_TEX_KINDS")) tx = std::max(tx, std::min(1, std::atoi(e)));
+    const KFn kf = stats ? fns_stats[mode] : fns[tx][lk][mode];
     const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;
