@@ -636,8 +636,14 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
         const float t02 = __builtin_fminf(qa2, qb2), t12 = __builtin_fmaxf(qa2, qb2);
         const float t1min = __builtin_fminf(__builtin_fminf(t10, t11), t12);
         const float t0max = __builtin_fmaxf(__builtin_fmaxf(t00, t01), t02);
-        const int hit_cond = (int)(te > ts) & (int)!(t1min <= ts) & (int)!(te <= t0max) & (int)(qa0 != qb0) &
-                             (int)(qa1 != qb1) & (int)(qa2 != qb2);
+        // hit_cond = te > ts && t1min > ts && t0max < te && qa_i != qb_i (i.e. t1_i > t0_i) for
+        // every axis.  All six are strict orderings x > y of non-NaN values (te may be +inf), and
+        // for those x > y <=> RN(x - y) > 0 (no difference of distinct floats rounds to zero;
+        // inf - finite = inf): one min over the six differences and one compare, instead of six
+        // compares whose masks the scalar unit would AND together.
+        const float dmin = __builtin_fminf(
+            __builtin_fminf(__builtin_fminf(te - ts, t1min - ts), te - t0max),
+            __builtin_fminf(__builtin_fminf(t10 - t00, t11 - t01), t12 - t02));
         // Given hit_cond, the cull's [max(ts, t0_i - w_i), min(te, t1_j + w_j)] is non-empty iff
         // max_i (t0_i - w_i) <= min_j (t1_j + w_j): ts <= te, ts < t1_j <= t1_j + w_j and
         // t0_i - w_i <= t0_i < te hold already (w_i >= 0).  A NaN delta (k = inf, D = 0, so every
@@ -646,7 +652,7 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
                     w2 = delta * __builtin_fabsf(rp.inv.z);
         const float lo = __builtin_fmaxf(__builtin_fmaxf(t00 - w0, t01 - w1), t02 - w2);
         const float hi = __builtin_fminf(__builtin_fminf(t10 + w0, t11 + w1), t12 + w2);
-        return hit_cond & (int)!(lo > hi);
+        return (int)(dmin > 0.0f) & (int)!(lo > hi);
     }
     const float qa0 = a0 / r.d.x, qb0 = b0 / r.d.x;
     const float qa1 = a1 / r.d.y, qb1 = b1 / r.d.y;
@@ -777,9 +783,11 @@ __device__ __forceinline__ float light_value(const rtw_rect& lg, V3 origin, V3 d
     return dsq / (cosine * area);
 }
 
-__device__ __forceinline__ V3 background(const rtw_background& bg, V3 d) {  // background_color.rs:9-19
+// background_color.rs:9-19; `pdot` = dot((0, 1, 0), d) of the primary ray, computed once per sample
+// (start_sample), so that a path carries one float instead of the direction
+__device__ __forceinline__ V3 background(const rtw_background& bg, float pdot) {
     if (bg.kind == RTW_BG_SKY) {
-        const float t = 0.5f * (dot(v3(0.0f, 1.0f, 0.0f), d) + 1.0f);
+        const float t = 0.5f * (pdot + 1.0f);
         return add(mul(v3(1.0f, 1.0f, 1.0f), 1.0f - t), mul(v3(0.5f, 0.7f, 1.0f), t));
     }
     return v3(bg.color[0], bg.color[1], bg.color[2]);
@@ -825,7 +833,7 @@ struct ShadeOut {
 
 template <bool STATS, int TX>
 __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t mode, Path P, int32_t found, float te,
-                                       V3 pdir) {
+                                       float pdot) {
     const DWorld& w = *wp;
     Stats st;
     st.c[ST_TEXEL] = 0;
@@ -939,7 +947,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
         }
     } else {
         // rendering.rs:67 (background of the PRIMARY ray) / :114
-        color = add(acc, conv(att, background(w.wc->bg, pdir)));
+        color = add(acc, conv(att, background(w.wc->bg, pdot)));
         done = true;
     }
     ShadeOut o;
@@ -1150,7 +1158,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     uint32_t pix = 0, slot = 0;
     float fx = 0.0f, fy = 0.0f;
     uint32_t sample = 0, sample_end = 0;
-    V3 pdir = v3(0.0f, 0.0f, 0.0f), att = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
+    float pdot = 0.0f;  // dot((0,1,0), primary ray direction): the background's argument
+    V3 att = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
     int32_t depth = 0;
     Trav T;
     T.phase = PH_PIXEL;
@@ -1170,7 +1179,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         const float jx = rtw_uniform_sample(&A.ux, &T.rng);
         const float jy = rtw_uniform_sample(&A.uy, &T.rng);
         T.ray = camera_ray(w.wc->cam, T.rng, fx + jx, fy + jy);
-        pdir = T.ray.d;
+        pdot = dot(v3(0.0f, 1.0f, 0.0f), T.ray.d);  // background_color.rs:13 on the primary ray
         att = v3(1.0f, 1.0f, 1.0f);
         acc = v3(0.0f, 0.0f, 0.0f);
         depth = A.max_depth;
@@ -1357,7 +1366,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             P.acc = acc;
             P.depth = depth;
             P.rng = T.rng;
-            const ShadeOut so = shade<STATS, TX>(A.wdev, A.mode, P, T.found, T.te, pdir);
+            const ShadeOut so = shade<STATS, TX>(A.wdev, A.mode, P, T.found, T.te, pdot);
             T.ray = so.p.ray;
             att = so.p.att;
             acc = so.p.acc;
