@@ -2133,7 +2133,8 @@ int grow(void** buf, size_t* have, size_t need) {
     return RTW_OK;
 }
 
-// One frame: launches of at most RTW_SAMPLE_BUFFER_BYTES (default 16 GiB) of per-sample colours,
+// One frame: launches of at most RTW_SAMPLE_BUFFER_BYTES (default: half of the HBM this world could
+// use, at most 64 GiB) of per-sample colours,
 // each followed by the in-order accumulation; work items of RTW_CHUNK (default 8) samples.
 // Launch l of a frame takes its work items from counter min(l, RTW_QUEUE_SLOTS - 1) of the
 // world's queue block, so a progress poller can read how many items each launch has handed out.
@@ -2157,7 +2158,16 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
                       std::vector<uint64_t>* launch_items) {
     if (A.total == 0) return RTW_OK;
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 1));
-    const size_t budget = env_size("RTW_SAMPLE_BUFFER_BYTES", (size_t)16 << 30);
+    // The colour buffer sets the launches per frame (C5, 4K x 2048 spp = 204 GB of colours: 13
+    // launches at a fixed 16 GiB, 4 at 64 GiB, one per rank of an 8-GPU split).  Default: half of
+    // the HBM this world could use (free memory plus the buffer it already holds), at most 64 GiB.
+    size_t budget = env_size("RTW_SAMPLE_BUFFER_BYTES", 0);
+    if (budget == 0) {
+        size_t free_b = 0, total_b = 0;
+        budget = (size_t)16 << 30;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            budget = std::min<size_t>((size_t)64 << 30, std::max<size_t>((size_t)1 << 30, (free_b + g->colors_bytes) / 2));
+    }
     const size_t per_sample = (size_t)A.total * 3 * sizeof(float);
     uint64_t per_launch = std::max<uint64_t>(chunk, (budget / per_sample) / chunk * chunk);
     per_launch = std::min<uint64_t>(per_launch, A.spp);
