@@ -966,7 +966,7 @@ extern __shared__ __attribute__((aligned(16))) float4 smem[];
 struct Trav {
     Ray ray;
     V3 inv;         // RN(1 / ray.d)
-    int32_t fast;   // Markstein division usable for this ray
+    int32_t fast;   // bits 0-2: ray.d[i] > 0 (the near child's side per axis); bit 3: Markstein division usable
     int32_t node;   // current node (>= 0) or ~leaf
     int32_t sp;
     float te;       // t_range.end, shrunk by every hit (hittable.rs:457)
@@ -1023,7 +1023,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
-    const RayPre rp{T.inv, T.fast != 0};
+    const RayPre rp{T.inv, (T.fast & 8) != 0};
     // execution counters, summed over lanes at the end: wave-level events are counted by the
     // first active lane of the wave (or of the branch) only
     uint32_t db[DB_SHADE_CALLS] = {};
@@ -1112,7 +1112,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 const int32_t left = lbits >> 2;
                 const int axis = lbits & 3;
                 const int32_t right = __float_as_int(nb.w);
-                const bool fwd = comp(T.ray.d, axis) > 0.0f;
+                const bool fwd = __builtin_amdgcn_ubfe((uint32_t)T.fast, (uint32_t)axis, 1u) != 0u;  // ray.d[axis] > 0
                 // hit_index_list order: near subtree, then far
                 stack[(T.sp++) * RTW_BLOCK] = fwd ? right : left;
                 T.node = fwd ? left : right;
@@ -1332,7 +1332,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             fresh = false;
             const RayPre rp = ray_pre(T.ray, A.mk_world != 0);
             T.inv = rp.inv;
-            T.fast = rp.fast ? 1 : 0;
+            T.fast = (rp.fast ? 8 : 0) | (T.ray.d.x > 0.0f ? 1 : 0) | (T.ray.d.y > 0.0f ? 2 : 0) | (T.ray.d.z > 0.0f ? 4 : 0);
             T.node = w.root;
             T.sp = 0;
             T.te = F32_INF;
