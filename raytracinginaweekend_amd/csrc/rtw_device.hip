@@ -170,6 +170,9 @@ struct KArgs {
     uint64_t big_from;          // items from here on are reserved RTW_WAVE_BATCH_BIG at a time
     // work-item decode (items < 2^32 per launch, render_frame): divisors as FastDiv
     FastDiv fd_total, fd_rank, fd_tile, fd_tiles_x, fd_tile_w;
+    // the refill's batch divisor (RTW_BATCH_SPREAD x waves) and the tuner's epoch / half-epoch:
+    // 64-bit divisions there expanded to ~140 instructions each
+    FastDiv fd_spread, fd_epoch, fd_half;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -993,11 +996,11 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 // LDS modes of the render kernel: 0 scene in HBM, 1 nodes + leaf records + cull constants + rect
 // records in LDS, 2 also the plain-triangle records (tri_fast).  LDS layout: [node_a n][node_b n]
 // [leaf_fast L][km ceil(n/2)][rects 2R][tri_fast 4T (mode 2)][stack depth x BLOCK]
-// Leaf kinds of the world (LK): 0 plain spheres only, 1 plain spheres / rects / triangles,
-// 2 any (wrapped leaves, boxes, volumes: the generic leaf path).  A world without generic leaves
-// gets a loop without that path: the generic path's rng update alone made the compiler copy the
-// lane's traversal registers at the leaf merge on every leaf step.
-enum { LK_SPHERES = 0, LK_PLAIN = 1, LK_ANY = 2 };
+// Leaf kinds of the world (LK): 0 plain spheres only, 1 plain spheres and triangles, 2 plain
+// spheres / rects / triangles, 3 any (wrapped leaves, boxes, volumes: the generic leaf path).  A
+// world without generic leaves gets a loop without that path: the generic path's rng update alone
+// made the compiler copy the lane's traversal registers at the leaf merge on every leaf step.
+enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_ANY = 3 };
 template <bool STATS, int LDS, int LK>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
                                       int32_t n_leaves, int32_t n_rects, int32_t n_tris, unsigned long long* dbg) {
@@ -1060,13 +1063,18 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 #endif
 #pragma unroll
         for (int u = 0; u < (STATS ? 1 : RTW_TRAV_UNROLL); ++u) {
-        if (T.phase == PH_TRACE && T.node < 0) {
+        // leaf bodies on every step, or (LK_SPHERES, LK_TRIS) on even steps only: a lane reaching a
+        // leaf then waits up to one step, and the wave runs a leaf body for twice the lanes half as
+        // often.  That pays where leaf steps are a small share (final_scene1 ~0.1 leaf per node
+        // step, suzanne ~0.4: +3 %, +5 %) and costs where leaves come at every turn (cornell_cube's
+        // wall rects, ~0.8: -8 %), hence only for worlds without rect, box or wrapped leaves.
+        if ((STATS || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == PH_TRACE && T.node < 0) {
             const int leaf = -1 - T.node;
             const float4 sph = fast[leaf];
             if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
                 if (STATS) st.c[ST_T_SPHERE]++;
                 sphere_leaf(sph, leaf, T.ray, T.te, T.found);
-            } else if (__float_as_int(sph.x) == 2) {  // a plain rect
+            } else if (LK >= LK_PLAIN && __float_as_int(sph.x) == 2) {  // a plain rect
                 if (STATS) st.c[ST_T_RECT]++;
                 const int ri = __float_as_int(sph.y);
                 const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
@@ -1077,7 +1085,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                     T.te = t;
                     T.found = leaf;
                 }
-            } else if (LK == LK_PLAIN || __float_as_int(sph.x) == 1) {  // a plain triangle
+            } else if (LK == LK_TRIS || LK == LK_PLAIN || __float_as_int(sph.x) == 1) {  // a plain triangle
                 if (STATS) st.c[ST_T_TRI]++;
                 float t;
                 if (tri_test(load_tri(tri_fast, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) {
@@ -1208,7 +1216,6 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     // wave's refills throttled fast-sample worlds); batches shrink toward the end of the launch so
     // that the last items still spread over all waves.
     uint64_t w_next = 0, w_end = 0;
-    const uint64_t n_waves = (uint64_t)gridDim.x * (RTW_BLOCK / 64);
     for (;;) {
         // 1. lanes without a pixel take the next items of the wave's reserve
         bool out_of_work = false;
@@ -1225,13 +1232,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 // small batches while the costly tiles are handed out: a wave slowed by long paths
                 // must not sit on a large reserve of them (an 8-GPU suzanne rank: 2.4x at 256)
                 const uint64_t cap = w_end >= A.big_from ? RTW_WAVE_BATCH_BIG : RTW_WAVE_BATCH;
-                const uint64_t batch = max(need - left, min(cap, rest / ((uint64_t)RTW_BATCH_SPREAD * n_waves)));
+                const uint64_t batch = max(need - left, min(cap, (uint64_t)fdiv((uint32_t)rest, A.fd_spread)));
                 unsigned long long b = 0;
                 if (lane == leader) b = atomicAdd(A.queue, (unsigned long long)batch);
                 base = __shfl(b, leader);
                 if (!tuned) {  // wave-uniform; the batch holding a half-epoch's first item stamps its start
-                    const uint64_t H = A.tune_items / 2;
-                    const uint64_t j = (base + H - 1) / H;
+                    const uint64_t H = A.fd_half.d;
+                    const uint64_t j = fdiv((uint32_t)(base + H - 1), A.fd_half);
                     if (lane == leader && j >= 1 && j <= RTW_TUNE_STAMPS && j * H < base + batch)
                         __hip_atomic_store(&A.tune->tb[j - 1], wall_clock64(), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
@@ -1241,8 +1248,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             const uint64_t first = w_next;
             w_next = (left < need) ? base + (need - left) : w_next + need;
             if (!tuned) {  // wave-uniform: the epoch of the items being handed out
-                const uint64_t E = A.tune_items;
-                const uint64_t e = w_next / E;
+                const uint64_t e = fdiv((uint32_t)w_next, A.fd_epoch);
                 if (e == 0) {
                     trace_min = A.trace_min;
                 } else if (e <= RTW_TUNE_EPOCHS) {
@@ -1941,8 +1947,11 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         if (w->textures[i].kind != RTW_TEX_SOLID) g->tex_kinds = TX_ANY;
     for (int i = 0; i < w->leaf_count; ++i) {
         const rtw_leaf& l = w->leaves[i];
-        if (l.flags != 0 || l.geom_kind == RTW_GEOM_BOX) g->leaf_kinds = LK_ANY;
-        else if (l.geom_kind != RTW_GEOM_SPHERE && g->leaf_kinds == LK_SPHERES) g->leaf_kinds = LK_PLAIN;
+        const int need = (l.flags != 0 || l.geom_kind == RTW_GEOM_BOX) ? LK_ANY
+                         : l.geom_kind == RTW_GEOM_RECT                 ? LK_PLAIN
+                         : l.geom_kind == RTW_GEOM_TRIANGLE             ? LK_TRIS
+                                                                        : LK_SPHERES;
+        g->leaf_kinds = std::max(g->leaf_kinds, (int32_t)need);
     }
     for (int i = 0; i < w->node_count; ++i)
         for (int k = 0; k < 3; ++k)
@@ -2065,15 +2074,16 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes : 0) + stack_bytes;
     using KFn = void (*)(KArgs);
 #define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}
-    static const KFn fns[2][3][3] = {{RTW_KSET(LK_SPHERES, TX_SOLID), RTW_KSET(LK_PLAIN, TX_SOLID), RTW_KSET(LK_ANY, TX_SOLID)},
-                                     {RTW_KSET(LK_SPHERES, TX_ANY), RTW_KSET(LK_PLAIN, TX_ANY), RTW_KSET(LK_ANY, TX_ANY)}};
+    static const KFn fns[2][4][3] = {
+        {RTW_KSET(LK_SPHERES, TX_SOLID), RTW_KSET(LK_TRIS, TX_SOLID), RTW_KSET(LK_PLAIN, TX_SOLID), RTW_KSET(LK_ANY, TX_SOLID)},
+        {RTW_KSET(LK_SPHERES, TX_ANY), RTW_KSET(LK_TRIS, TX_ANY), RTW_KSET(LK_PLAIN, TX_ANY), RTW_KSET(LK_ANY, TX_ANY)}};
 #undef RTW_KSET
     static const KFn fns_stats[3] = {render_kernel<true, 0, LK_ANY, TX_ANY>, render_kernel<true, 1, LK_ANY, TX_ANY>,
                                      render_kernel<true, 2, LK_ANY, TX_ANY>};
-    // the leaf and texture kinds the world needs; RTW_LEAF_KINDS=2 / RTW_TEX_KINDS=1 force the
+    // the leaf and texture kinds the world needs; RTW_LEAF_KINDS=3 / RTW_TEX_KINDS=1 force the
     // generic code (audits)
     int lk = g->leaf_kinds, tx = g->tex_kinds;
-    if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(2, std::atoi(e)));
+    if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(3, std::atoi(e)));
     if (const char* e = std::getenv("RTW_TEX_KINDS")) tx = std::max(tx, std::min(1, std::atoi(e)));
     const KFn kf = stats ? fns_stats[mode] : fns[tx][lk][mode];
     const void* fn = (const void*)kf;
@@ -2096,6 +2106,9 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
             HIP_TRY(hipMemsetAsync(A.tune->tb, 0xFF, sizeof(A.tune->tb), stream));
         }
     }
+    A.fd_spread = fastdiv_make((uint32_t)(RTW_BATCH_SPREAD * blocks * (RTW_BLOCK / 64)));
+    A.fd_epoch = fastdiv_make((uint32_t)std::max<uint64_t>(1, A.tune_items));
+    A.fd_half = fastdiv_make((uint32_t)std::max<uint64_t>(1, A.tune_items / 2));
     hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
     HIP_TRY(hipGetLastError());
     return RTW_OK;
