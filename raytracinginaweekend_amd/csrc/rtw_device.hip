@@ -963,6 +963,19 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
 
 enum { PH_PIXEL = 0, PH_TRACE = 1, PH_SHADE = 2 };
 
+// Experiment builds only (make variant DEFS=-DRTW_PHASE_TIMING): per-wave wall cycles of the main
+// loop's phases, summed over waves into rtw_phase_cycles (read by rtw_debug_phase_cycles).
+#ifdef RTW_PHASE_TIMING
+__device__ unsigned long long rtw_phase_cycles[8];
+#define RTW_PT_DECL uint64_t pt_last = clock64(); uint64_t pt_acc[8] = {}; int pt_cur = 0;
+#define RTW_PT(k) do { const uint64_t now_ = clock64(); pt_acc[pt_cur] += now_ - pt_last; pt_last = now_; pt_cur = (k); } while (0)
+#define RTW_PT_FLUSH do { RTW_PT(0); if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&rtw_phase_cycles[k_], (unsigned long long)pt_acc[k_]); } while (0)
+#else
+#define RTW_PT_DECL
+#define RTW_PT(k) do { } while (0)
+#define RTW_PT_FLUSH do { } while (0)
+#endif
+
 extern __shared__ __attribute__((aligned(16))) float4 smem[];
 
 // Traversal state of one lane (by value, in registers, across the out-of-line call).
@@ -1216,8 +1229,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     // wave's refills throttled fast-sample worlds); batches shrink toward the end of the launch so
     // that the last items still spread over all waves.
     uint64_t w_next = 0, w_end = 0;
+    RTW_PT_DECL
     for (;;) {
         // 1. lanes without a pixel take the next items of the wave's reserve
+        RTW_PT(1);
         bool out_of_work = false;
         for (;;) {
             const unsigned long long m = __ballot(T.phase == PH_PIXEL);
@@ -1328,6 +1343,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         if (out_of_work) break;
 
         // 2. a new ray starts at the root (Scene::hit with t_range 0.001..inf, rendering.rs:25)
+        RTW_PT(2);
         uint64_t c_trav = 0;
         if (STATS) {
             c_trav = clock64();
@@ -1347,6 +1363,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
 
         // 3. traversal (hittable.rs:429-473)
+        RTW_PT(3);
         T = traverse<STATS, LDS, LK>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, A.leaf_count,
                                  A.rect_count, A.tri_count,
                                        STATS ? A.stats + ST_COUNT : nullptr);
@@ -1364,6 +1381,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
 
         // 4. shade the lanes whose traversal finished (rendering.rs:19-71)
+        RTW_PT(4);
         if (STATS) {
             const unsigned long long sm = __ballot(T.phase == PH_SHADE);
             if (sm && lane == __ffsll((long long)__ballot(1)) - 1) {
@@ -1408,6 +1426,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             }
         }
     }
+    RTW_PT_FLUSH;
     if (STATS) {
         for (int i = 0; i < ST_COUNT; ++i)
             if (st.c[i]) atomicAdd(&A.stats[i], (unsigned long long)st.c[i]);
@@ -1734,6 +1753,20 @@ struct rtw_gpu_world {
     uint32_t order_tiles = 0;
     bool order_valid = false;      // tile permutation computed for order_key
 };
+
+// experiment builds (-DRTW_PHASE_TIMING): read and reset the phase cycle sums
+extern "C" RTW_API int rtw_debug_phase_cycles(unsigned long long* out8) {
+#ifdef RTW_PHASE_TIMING
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(rtw_phase_cycles), 8 * sizeof(unsigned long long)));
+    unsigned long long z[8] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rtw_phase_cycles), z, sizeof(z)));
+    return RTW_OK;
+#else
+    (void)out8;
+    return rtw::fail(RTW_ERR_UNSUPPORTED, "built without RTW_PHASE_TIMING");
+#endif
+}
 
 extern "C" RTW_API int rtw_device_count(int* count) {
     if (!count) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null count");
