@@ -4,7 +4,7 @@
 #   GPU (C4 suzanne, C3 cornell_cube, C5 earth_motion), one rank's share of 8-GPU splits, and
 #   PMC passes of the render kernel (final_scene1, suzanne).
 set -o pipefail
-O=gpurun_out/r02; mkdir -p $O
+O=gpurun_out/${ROUND_TAG:-r02}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
