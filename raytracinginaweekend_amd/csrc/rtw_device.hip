@@ -440,13 +440,15 @@ __device__ __forceinline__ Ray leaf_local_ray(const DWorld& w, int leaf, uint32_
 }
 
 // SceneElement::hit for one leaf (candidate test: t only).  Volumes draw one f32 here.
-template <bool STATS>
+// VOL: the world may hold volume leaves (the only leaves that draw from the path's RNG during the
+// traversal); without them the RNG state never changes inside the loop
+template <bool STATS, bool VOL = true>
 __device__ __forceinline__ bool leaf_t(const DWorld& w, int leaf, const Ray& r, float ts, float te, rtw_xoro& rng,
                                        float& t, Stats& st) {
     const int4 info = w.leaf_info[leaf];
     const uint32_t flags = (uint32_t)info.w;
     const Ray rr = (flags & (RTW_LEAF_ANIMATION | RTW_LEAF_TRANSFORM)) ? leaf_local_ray(w, leaf, flags, r) : r;
-    const bool volume = (flags & RTW_LEAF_VOLUME) != 0;
+    const bool volume = VOL && (flags & RTW_LEAF_VOLUME) != 0;
     // VolumeGeometry::hit (hittable.rs:309-331): boundary hit over (-inf, inf), then from t0+0.001
     float lo = volume ? -F32_INF : ts, hi = volume ? F32_INF : te;
     float t0 = 0.0f;
@@ -1010,10 +1012,12 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 // records in LDS, 2 also the plain-triangle records (tri_fast).  LDS layout: [node_a n][node_b n]
 // [leaf_fast L][km ceil(n/2)][rects 2R][tri_fast 4T (mode 2)][stack depth x BLOCK]
 // Leaf kinds of the world (LK): 0 plain spheres only, 1 plain spheres and triangles, 2 plain
-// spheres / rects / triangles, 3 any (wrapped leaves, boxes, volumes: the generic leaf path).  A
-// world without generic leaves gets a loop without that path: the generic path's rng update alone
-// made the compiler copy the lane's traversal registers at the leaf merge on every leaf step.
-enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_ANY = 3 };
+// spheres / rects / triangles, 3 wrapped leaves and boxes too (the generic leaf path without
+// volumes), 4 any (volumes: the generic path draws from the RNG).  A world without generic leaves
+// gets a loop without that path, and one without volumes a generic path that leaves the RNG alone:
+// the RNG update alone made the compiler copy the lane's traversal registers at the leaf merge on
+// every leaf step.
+enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_WRAPPED = 3, LK_ANY = 4 };
 template <bool STATS, int LDS, int LK>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
                                       int32_t n_leaves, int32_t n_rects, int32_t n_tris, unsigned long long* dbg) {
@@ -1105,9 +1109,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                     T.te = t;
                     T.found = leaf;
                 }
-            } else if (LK == LK_ANY) {
+            } else if (LK >= LK_WRAPPED) {
                 float t;
-                if (leaf_t<STATS>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) {
+                if (leaf_t<STATS, LK == LK_ANY>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) {
                     T.te = t;
                     T.found = leaf;
                 }
@@ -1980,7 +1984,8 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         if (w->textures[i].kind != RTW_TEX_SOLID) g->tex_kinds = TX_ANY;
     for (int i = 0; i < w->leaf_count; ++i) {
         const rtw_leaf& l = w->leaves[i];
-        const int need = (l.flags != 0 || l.geom_kind == RTW_GEOM_BOX) ? LK_ANY
+        const int need = (l.flags & RTW_LEAF_VOLUME)                   ? LK_ANY
+                         : (l.flags != 0 || l.geom_kind == RTW_GEOM_BOX) ? LK_WRAPPED
                          : l.geom_kind == RTW_GEOM_RECT                 ? LK_PLAIN
                          : l.geom_kind == RTW_GEOM_TRIANGLE             ? LK_TRIS
                                                                         : LK_SPHERES;
@@ -2107,16 +2112,18 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes : 0) + stack_bytes;
     using KFn = void (*)(KArgs);
 #define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}
-    static const KFn fns[2][4][3] = {
-        {RTW_KSET(LK_SPHERES, TX_SOLID), RTW_KSET(LK_TRIS, TX_SOLID), RTW_KSET(LK_PLAIN, TX_SOLID), RTW_KSET(LK_ANY, TX_SOLID)},
-        {RTW_KSET(LK_SPHERES, TX_ANY), RTW_KSET(LK_TRIS, TX_ANY), RTW_KSET(LK_PLAIN, TX_ANY), RTW_KSET(LK_ANY, TX_ANY)}};
+    static const KFn fns[2][5][3] = {
+        {RTW_KSET(LK_SPHERES, TX_SOLID), RTW_KSET(LK_TRIS, TX_SOLID), RTW_KSET(LK_PLAIN, TX_SOLID),
+         RTW_KSET(LK_WRAPPED, TX_SOLID), RTW_KSET(LK_ANY, TX_SOLID)},
+        {RTW_KSET(LK_SPHERES, TX_ANY), RTW_KSET(LK_TRIS, TX_ANY), RTW_KSET(LK_PLAIN, TX_ANY),
+         RTW_KSET(LK_WRAPPED, TX_ANY), RTW_KSET(LK_ANY, TX_ANY)}};
 #undef RTW_KSET
     static const KFn fns_stats[3] = {render_kernel<true, 0, LK_ANY, TX_ANY>, render_kernel<true, 1, LK_ANY, TX_ANY>,
                                      render_kernel<true, 2, LK_ANY, TX_ANY>};
-    // the leaf and texture kinds the world needs; RTW_LEAF_KINDS=3 / RTW_TEX_KINDS=1 force the
+    // the leaf and texture kinds the world needs; RTW_LEAF_KINDS=4 / RTW_TEX_KINDS=1 force the
     // generic code (audits)
     int lk = g->leaf_kinds, tx = g->tex_kinds;
-    if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(3, std::atoi(e)));
+    if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RTW_TEX_KINDS")) tx = std::max(tx, std::min(1, std::atoi(e)));
     const KFn kf = stats ? fns_stats[mode] : fns[tx][lk][mode];
     const void* fn = (const void*)kf;

@@ -108,16 +108,16 @@ def test_tile_partitions_reassemble_bit_exact(worlds, name, world_size):
     assert_bit_identical(host, full, "untile_host")
 
 
-@pytest.mark.parametrize("name", ["final_scene1", "suzanne", "cornell_cube"])
+@pytest.mark.parametrize("name", ["final_scene1", "suzanne", "cornell_cube", "earth_motion", "cornell_box"])
 def test_leaf_kind_loops_agree(worlds, name, monkeypatch):
     """The traversal loop specialised to the world's leaf kinds (plain spheres only / plain
-    spheres and triangles, or with rects) gives the generic loop's bits (RTW_LEAF_KINDS=3) on a frame
+    spheres and triangles, or with rects) gives the generic loop's bits (RTW_LEAF_KINDS=4) on a frame
     large enough to fill the GPU, and the oracle's on a small one."""
     world = worlds(name)
     size = R.Size2i(320, 180)
     fast = R.render(size, 1, 8, 50, world, seed=21)
     small = R.render(R.Size2i(40, 24), 1, 4, 50, world, seed=21)
-    monkeypatch.setenv("RTW_LEAF_KINDS", "3")
+    monkeypatch.setenv("RTW_LEAF_KINDS", "4")
     generic = R.render(size, 1, 8, 50, world, seed=21)
     assert_bit_identical(fast, generic, name + " specialised vs generic loop")
     assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(40, 24), 4, 50, seed=21)), name)
