@@ -621,6 +621,9 @@ __device__ __forceinline__ RayPre ray_pre(const Ray& r, bool mk_world) {
 
 // Aabb::hit_cond (exact quotients) AND the proximity cull (rtw_scalar.h rtw_cull_*), which
 // reuses the same quotients: pass iff the segment [ts, te] meets the box grown by delta.
+// FAST_ONLY: every ray of the call is Markstein-exact (render_body picks the loop per traversal
+// call), so the true-division path and its per-lane branch are compiled out of the loop
+template <bool FAST_ONLY = false>
 __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const Ray& r, const RayPre& rp, float ts,
                                           float te) {
     const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
@@ -630,7 +633,7 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
     const float dsum = ((__builtin_fabsf(a0) + __builtin_fabsf(b0)) + (__builtin_fabsf(a1) + __builtin_fabsf(b1))) +
                        (__builtin_fabsf(a2) + __builtin_fabsf(b2));
     const float delta = rtw_cull_delta(km.x, km.y, dsum);
-    if (__builtin_expect(rp.fast, 1)) {
+    if (FAST_ONLY || __builtin_expect(rp.fast, 1)) {
         const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
         const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
         const float qa2 = mk_div(a2, r.d.z, rp.inv.z), qb2 = mk_div(b2, r.d.z, rp.inv.z);
@@ -1018,7 +1021,7 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 // the RNG update alone made the compiler copy the lane's traversal registers at the leaf merge on
 // every leaf step.
 enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_WRAPPED = 3, LK_ANY = 4 };
-template <bool STATS, int LDS, int LK>
+template <bool STATS, int LDS, int LK, bool FAST_ONLY>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
                                       int32_t n_leaves, int32_t n_rects, int32_t n_tris, unsigned long long* dbg) {
     constexpr bool LDS_SCENE = LDS >= 1;
@@ -1131,7 +1134,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             const float4 na = nodes_a[T.node];
             const float4 nb = nodes_b[T.node];
             const float2 km = nkm[T.node];
-            if (node_pass(na, nb, km, T.ray, rp, 0.001f, T.te)) {
+            if (node_pass<FAST_ONLY>(na, nb, km, T.ray, rp, 0.001f, T.te)) {
                 if (STATS) db[DB_PASS_LANES]++;
                 const int32_t lbits = __float_as_int(nb.z);
                 const int32_t left = lbits >> 2;
@@ -1368,9 +1371,16 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 
         // 3. traversal (hittable.rs:429-473)
         RTW_PT(3);
-        T = traverse<STATS, LDS, LK>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, A.leaf_count,
-                                 A.rect_count, A.tri_count,
-                                       STATS ? A.stats + ST_COUNT : nullptr);
+        // (almost) every ray is Markstein-exact: such calls run a loop without the true-division
+        // path (wave-uniform choice per call)
+        if (__ballot(T.phase == PH_TRACE && (T.fast & 8) == 0) == 0)
+            T = traverse<STATS, LDS, LK, true>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
+                                               A.leaf_count, A.rect_count, A.tri_count,
+                                               STATS ? A.stats + ST_COUNT : nullptr);
+        else
+            T = traverse<STATS, LDS, LK, false>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
+                                                A.leaf_count, A.rect_count, A.tri_count,
+                                                STATS ? A.stats + ST_COUNT : nullptr);
         if (STATS) {
             c_mark = clock64();
             if (lane == __ffsll((long long)__ballot(1)) - 1)
