@@ -2005,6 +2005,10 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         for (int k = 0; k < 3; ++k)
             for (float c : {w->nodes[i].min[k], w->nodes[i].max[k]})
                 if (!(c == 0.0f || std::fabs(c) >= 0x1p-60f)) g->mk_world = 0;
+    // audits: RTW_NO_MARKSTEIN=1 makes every ray take the true-division slab test (and the traversal
+    // loop that carries it)
+    if (const char* e = std::getenv("RTW_NO_MARKSTEIN"))
+        if (e[0] && e[0] != '0') g->mk_world = 0;
     (void)hipDeviceGetAttribute(&g->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (g->cus <= 0) g->cus = 256;
     {

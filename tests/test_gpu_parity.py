@@ -123,6 +123,34 @@ def test_leaf_kind_loops_agree(worlds, name, monkeypatch):
     assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(40, 24), 4, 50, seed=21)), name)
 
 
+@pytest.mark.parametrize("name", ["final_scene1", "suzanne"])
+def test_true_division_loop_agrees(worlds, name, monkeypatch):
+    """Every ray on the true-division slab test (the general traversal loop, RTW_NO_MARKSTEIN=1)
+    gives the Markstein loop's bits on a GPU-filling frame, and the oracle's on a small one."""
+    world = worlds(name)
+    size = R.Size2i(320, 180)
+    fast = R.render(size, 1, 8, 50, world, seed=23)
+    monkeypatch.setenv("RTW_NO_MARKSTEIN", "1")
+    slow = R.render(size, 1, 8, 50, world, seed=23)
+    small = R.render(R.Size2i(40, 24), 1, 4, 50, world, seed=23)
+    assert_bit_identical(fast, slow, name + " Markstein vs true-division loop")
+    assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(40, 24), 4, 50, seed=23)), name)
+
+
+@pytest.mark.parametrize("name", ["final_scene1", "suzanne"])
+def test_true_division_loop_agrees(worlds, name, monkeypatch):
+    """Every ray on the true-division slab test (the general traversal loop, RTW_NO_MARKSTEIN=1)
+    gives the Markstein loop's bits on a GPU-filling frame, and the oracle's on a small one."""
+    world = worlds(name)
+    size = R.Size2i(320, 180)
+    fast = R.render(size, 1, 8, 50, world, seed=23)
+    monkeypatch.setenv("RTW_NO_MARKSTEIN", "1")
+    slow = R.render(size, 1, 8, 50, world, seed=23)
+    small = R.render(R.Size2i(40, 24), 1, 4, 50, world, seed=23)
+    assert_bit_identical(fast, slow, name + " Markstein vs true-division loop")
+    assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(40, 24), 4, 50, seed=23)), name)
+
+
 def test_progress_callback_reports_and_keeps_bits(worlds):
     """rtw_render_progress (the reference's progress thread, rendering.rs:140-157): monotone
     (done, total) reports ending at total, and the image equals rtw_render's."""
