@@ -399,6 +399,7 @@ def main() -> int:
                 "partition": f"interleaved {spec.tile[0]}x{spec.tile[1]} tiles over {world_size} GPU(s)",
                 "rccl_world_size": world_size,
                 "trace_min": fr.dworld.tuned_trace_min(),
+                "kernel": fr.dworld.kernel_variant(),
             },
             "first_frame_ms": first_frame_ms,
             "roofline": roofline,

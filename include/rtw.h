@@ -263,6 +263,11 @@ RTW_API int rtw_world_release(rtw_gpu_world* gw);
  * the first long render; 0 while still exploring).  Synchronous; performance only -- images do
  * not depend on it. */
 RTW_API int rtw_world_tuning(rtw_gpu_world* gw, int* trace_min);
+/* The render-kernel variant this world's last render launched: LDS mode (0 scene in HBM, 1 BVH +
+ * leaf records in LDS, 2 + triangle records), leaf kinds (0 plain spheres ..
+ * 4 any) and texture kinds (0 solid only, 1 any); -1 each before the first render.  Diagnostics
+ * only. */
+RTW_API int rtw_world_kernel(rtw_gpu_world* gw, int* lds_mode, int* leaf_kinds, int* tex_kinds);
 /* Renders this partition's tiles into device buffer `d_out` (layout per params->layout) on
  * `stream` (a hipStream_t, NULL = default stream).  Asynchronous: returns after the launch. */
 RTW_API int rtw_render_device(rtw_gpu_world* gw, const rtw_render_params* params, float* d_out,

@@ -1766,6 +1766,7 @@ struct rtw_gpu_world {
     bool done_recorded = false;
     uint32_t order_tiles = 0;
     bool order_valid = false;      // tile permutation computed for order_key
+    int32_t last_kernel[3] = {-1, -1, -1};  // LDS mode, leaf kinds, texture kinds of the last render
 };
 
 // experiment builds (-DRTW_PHASE_TIMING): read and reset the phase cycle sums
@@ -2039,6 +2040,14 @@ extern "C" RTW_API int rtw_world_tuning(rtw_gpu_world* g, int* trace_min) {
     return RTW_OK;
 }
 
+extern "C" RTW_API int rtw_world_kernel(rtw_gpu_world* g, int* lds_mode, int* leaf_kinds, int* tex_kinds) {
+    if (!g || !lds_mode || !leaf_kinds || !tex_kinds) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    *lds_mode = g->last_kernel[0];
+    *leaf_kinds = g->last_kernel[1];
+    *tex_kinds = g->last_kernel[2];
+    return RTW_OK;
+}
+
 extern "C" RTW_API int rtw_world_release(rtw_gpu_world* g) {
     if (!g) return RTW_OK;
     (void)hipSetDevice(g->device);
@@ -2140,6 +2149,11 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RTW_TEX_KINDS")) tx = std::max(tx, std::min(1, std::atoi(e)));
     const KFn kf = stats ? fns_stats[mode] : fns[tx][lk][mode];
+    if (!stats) {
+        g->last_kernel[0] = mode;
+        g->last_kernel[1] = lk;
+        g->last_kernel[2] = tx;
+    }
     const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;

@@ -125,6 +125,12 @@ class DeviceWorld:
         check(lib().rtw_world_tuning(self._h, C.byref(v)))
         return v.value
 
+    def kernel_variant(self) -> dict:
+        """The render-kernel variant of the last render (LDS mode, leaf kinds, texture kinds)."""
+        m, lk, tx = C.c_int(), C.c_int(), C.c_int()
+        check(lib().rtw_world_kernel(self._h, C.byref(m), C.byref(lk), C.byref(tx)))
+        return {"lds_mode": m.value, "leaf_kinds": lk.value, "tex_kinds": tx.value}
+
     def collect_stats(self, params: N.RenderParams) -> dict:
         s = N.RenderStats()
         check(lib().rtw_render_collect_stats(self._h, C.byref(params), C.byref(s)))
