@@ -263,11 +263,12 @@ RTW_API int rtw_world_release(rtw_gpu_world* gw);
  * the first long render; 0 while still exploring).  Synchronous; performance only -- images do
  * not depend on it. */
 RTW_API int rtw_world_tuning(rtw_gpu_world* gw, int* trace_min);
-/* The render-kernel variant this world's last render launched: LDS mode (0 scene in HBM, 1 BVH +
- * leaf records in LDS, 2 + triangle records), leaf kinds (0 plain spheres ..
- * 4 any) and texture kinds (0 solid only, 1 any); -1 each before the first render.  Diagnostics
- * only. */
-RTW_API int rtw_world_kernel(rtw_gpu_world* gw, int* lds_mode, int* leaf_kinds, int* tex_kinds);
+/* The render-kernel variant this world's last render launched: LDS mode (0 scene in HBM, 1 tree +
+ * leaf records in LDS, 2 + triangle records), leaf kinds (0 plain spheres .. 4 any), texture
+ * kinds (0 solid only, 1 any) and search tree (0 the reference BVH, 1 the kernel's SAH tree with
+ * the reference-order proof and fallback); -1 each before the first render.
+ * Diagnostics only. */
+RTW_API int rtw_world_kernel(rtw_gpu_world* gw, int* lds_mode, int* leaf_kinds, int* tex_kinds, int* tree);
 /* Renders this partition's tiles into device buffer `d_out` (layout per params->layout) on
  * `stream` (a hipStream_t, NULL = default stream).  Asynchronous: returns after the launch. */
 RTW_API int rtw_render_device(rtw_gpu_world* gw, const rtw_render_params* params, float* d_out,
@@ -306,6 +307,10 @@ RTW_API int rtw_device_eval_scalar(int device, int fn, const float* a, const flo
  * (1: node coordinates admit the per-ray exact-division guard).  out[i] = 1 if the node passes. */
 RTW_API int rtw_device_eval_node_pass(int device, const float* box, const float* ray, const float* range,
                                       const float* km, int32_t mk_world, int64_t n, int32_t* out);
+
+/* Device self-test of CheckerTexture's sign test (texture.rs:33-40) as the render kernel evaluates
+ * it: out[i] = 1 if RN(RN(sinf(x) sinf(y)) sinf(z)) < 0 for (x, y, z) = xyz[3i..3i+2], else 0. */
+RTW_API int rtw_device_eval_checker(int device, const float* xyz, int64_t n, int32_t* out);
 
 /* ---- host scene construction ------------------------------------------------------------- */
 typedef struct rtw_builder rtw_builder;         /* WorldBuilder + arena (world_builder.rs:7-14) */

@@ -242,7 +242,7 @@ _SIGS = {
     "rtw_world_upload": (C.c_int, [C.POINTER(World), C.c_int, C.POINTER(_P)]),
     "rtw_world_release": (C.c_int, [_P]),
     "rtw_world_tuning": (C.c_int, [_P, C.POINTER(C.c_int)]),
-    "rtw_world_kernel": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "rtw_world_kernel": (C.c_int, [_P] + [C.POINTER(C.c_int)] * 4),
     "rtw_render_device": (C.c_int, [_P, C.POINTER(RenderParams), _P, _P]),
     "rtw_partition_floats": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int64)]),
     "rtw_untile_device": (C.c_int, [C.POINTER(RenderParams), _P, C.c_int64, _P, _P]),
@@ -256,6 +256,7 @@ _SIGS = {
         C.c_int,
         [C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_float)],
     ),
+    "rtw_device_eval_checker": (C.c_int, [C.c_int, C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_int32)]),
     "rtw_device_eval_node_pass": (
         C.c_int,
         [C.c_int] + [C.POINTER(C.c_float)] * 4 + [C.c_int32, C.c_int64, C.POINTER(C.c_int32)],

@@ -4,6 +4,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include <hip/hip_runtime_api.h>
 
@@ -26,5 +27,10 @@ const char* last_error();
 // only sets *tmp_bytes.
 hipError_t sort_pairs_desc(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in, uint32_t* vals_out,
                            int n, void* tmp, size_t* tmp_bytes, hipStream_t stream);
+
+// The render kernel's surface-area-heuristic tree over n leaf boxes (lo/hi: 3 floats per leaf),
+// children encoded as in rtw_bvh_node (>= 0 node, < 0 leaf -1 - index).  *depth = nodes on the
+// longest root-to-leaf path (rtw_sah.cpp).
+int sah_build(const float* lo, const float* hi, int32_t n, std::vector<rtw_bvh_node>& nodes, int32_t* root, int* depth);
 
 }  // namespace rtw

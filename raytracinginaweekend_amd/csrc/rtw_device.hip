@@ -23,6 +23,7 @@
 #include <cstring>
 #include <ctime>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rtw_scalar.h"
@@ -77,6 +78,13 @@ struct DWorld {
     const uint32_t* perlin_perm; // 768 per perlin (x, y, z)
     const int* perlin_bits;
     const struct WorldConst* wc; // camera / light / background, read from memory when used
+    // the kernel's own search tree (rtw_sah.cpp; node format of node_a / node_b) and each leaf's
+    // Aabb (2 per leaf: {min.xyz, max.x}, {max.y, max.z, 0, 0}) for the verification (§5.6)
+    const float4* sah_a;
+    const float4* sah_b;
+    const float2* sah_km;
+    const float4* leaf_box;
+    int32_t sah_root;
     int32_t root;
     int32_t has_light;
 };
@@ -162,6 +170,8 @@ struct KArgs {
     unsigned long long* stats; // 13 counters (stats variant only)
     TuneState* tune;          // in-frame threshold tuning, or null
     int32_t mk_world;         // node coordinates admit the per-ray exact-division guard (ray_pre)
+    int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
+                              // re-traced on the reference tree where the proof does not hold (§5.6)
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
     // work order by measured cost (render_frame): costlier tiles first, all their samples together
     const uint32_t* tile_perm;  // tile rank -> local tile, null: chunk-major order
@@ -219,6 +229,29 @@ __device__ __noinline__ float d_acosf(float x) { return rtw_acosf(x); }
 __device__ __noinline__ float d_atan2f(float y, float x) { return rtw_atan2f(y, x); }
 __device__ __noinline__ float d_logf(float x) { return rtw_logf(x); }
 __device__ __noinline__ float d_sinf(float x) { return rtw_sinf(x); }
+
+// CheckerTexture's test (texture.rs:33-40): is RN(RN(sinf(x) * sinf(y)) * sinf(z)) < 0?  Only the
+// sign of the product is read, so the sines' polynomials are not needed when rtw_sinf's own
+// reduction (x = k pi/2 + r, exact for |x| < 2^19) leaves |r| > 2^-30: each sine then has the sign
+// its quadrant and r give (sin r for k = 0 mod 4, cos r > 0 for 1, -sin r for 2, -cos r for 3;
+// |r| <= pi/4) and magnitude > 2^-31, so neither f32 product is zero, subnormal or of another
+// sign, and the result is negative iff an odd number of the sines are.  Other arguments (0,
+// huge, NaN, near a multiple of pi) evaluate the sines.
+__device__ __noinline__ bool d_checker_odd(float x, float y, float z) {
+    const float c[3] = {x, y, z};
+    bool fast = true, odd = false;
+    for (int i = 0; i < 3; ++i) {
+        const double d = (double)c[i];
+        const double kd = __builtin_rint(d * 0.63661977236758138243);
+        const double r = ((d - kd * 1.57079632673412561417e+00) - kd * 6.07710050630396597660e-11) -
+                         kd * 2.02226624871116645580e-21;
+        fast = fast && __builtin_fabs(d) < 0x1p19 && __builtin_fabs(r) > 0x1p-30;
+        const int q = (int)kd & 3;  // |kd| < 2^19 on the fast path
+        odd ^= (q == 0) ? r < 0.0 : (q == 2) ? r > 0.0 : q == 3;
+    }
+    if (fast) return odd;
+    return d_sinf(x) * d_sinf(y) * d_sinf(z) < 0.0f;
+}
 
 struct Ray {
     V3 o, d;
@@ -684,6 +717,50 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
     return hit_cond & (int)(clo <= chi);
 }
 
+// The SAH tree's node test: the proximity cull alone (fast rays only), i.e. the segment [ts, te]
+// meets the box grown by delta.  Conservative: never rejects a node below which a leaf's test
+// would accept a root in [ts, te) (§5.2), whatever the tree.  A NaN delta (k = inf, D = 0) drops
+// out of the bounds, as in rtw_cull_axis.
+__device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, const Ray& r, const RayPre& rp, float ts,
+                                               float te) {
+    const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
+    const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
+    const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
+    const float dsum = ((__builtin_fabsf(a0) + __builtin_fabsf(b0)) + (__builtin_fabsf(a1) + __builtin_fabsf(b1))) +
+                       (__builtin_fabsf(a2) + __builtin_fabsf(b2));
+    const float delta = rtw_cull_delta(km.x, km.y, dsum);
+    const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
+    const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
+    const float qa2 = mk_div(a2, r.d.z, rp.inv.z), qb2 = mk_div(b2, r.d.z, rp.inv.z);
+    const float w0 = delta * __builtin_fabsf(rp.inv.x), w1 = delta * __builtin_fabsf(rp.inv.y),
+                w2 = delta * __builtin_fabsf(rp.inv.z);
+    const float lo = __builtin_fmaxf(
+        __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(qa0, qb0) - w0, __builtin_fminf(qa1, qb1) - w1),
+                        __builtin_fminf(qa2, qb2) - w2),
+        ts);
+    const float hi = __builtin_fminf(
+        __builtin_fminf(__builtin_fminf(__builtin_fmaxf(qa0, qb0) + w0, __builtin_fmaxf(qa1, qb1) + w1),
+                        __builtin_fmaxf(qa2, qb2) + w2),
+        te);
+    return !(lo > hi);
+}
+
+// Aabb::hit_cond (aabb.rs:65-78) alone, exact quotients (fast rays only): node_pass's first half
+__device__ __forceinline__ bool box_hit_cond_fast(float4 na, float4 nb, const Ray& r, const RayPre& rp, float ts,
+                                                  float te) {
+    const float qa0 = mk_div(na.x - r.o.x, r.d.x, rp.inv.x), qb0 = mk_div(na.w - r.o.x, r.d.x, rp.inv.x);
+    const float qa1 = mk_div(na.y - r.o.y, r.d.y, rp.inv.y), qb1 = mk_div(nb.x - r.o.y, r.d.y, rp.inv.y);
+    const float qa2 = mk_div(na.z - r.o.z, r.d.z, rp.inv.z), qb2 = mk_div(nb.y - r.o.z, r.d.z, rp.inv.z);
+    const float t00 = __builtin_fminf(qa0, qb0), t10 = __builtin_fmaxf(qa0, qb0);
+    const float t01 = __builtin_fminf(qa1, qb1), t11 = __builtin_fmaxf(qa1, qb1);
+    const float t02 = __builtin_fminf(qa2, qb2), t12 = __builtin_fmaxf(qa2, qb2);
+    const float t1min = __builtin_fminf(__builtin_fminf(t10, t11), t12);
+    const float t0max = __builtin_fmaxf(__builtin_fmaxf(t00, t01), t02);
+    const float dmin = __builtin_fminf(__builtin_fminf(__builtin_fminf(te - ts, t1min - ts), te - t0max),
+                                       __builtin_fminf(__builtin_fminf(t10 - t00, t11 - t01), t12 - t02));
+    return dmin > 0.0f;
+}
+
 // ---------------------------------------------------------------------------------------------
 // textures / materials / light / background
 // ---------------------------------------------------------------------------------------------
@@ -737,8 +814,7 @@ __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit
         if (kind == RTW_TEX_CHECKER) {
             const float f = __int_as_float(t1.x);
             const V3 s = mul(h.pos, f);
-            const float sines = d_sinf(s.x) * d_sinf(s.y) * d_sinf(s.z);
-            tex = (sines < 0.0f) ? t1.y : t1.z;
+            tex = d_checker_odd(s.x, s.y, s.z) ? t1.y : t1.z;  // sines < 0
             continue;
         }
         const int4 t2 = w.textures[3 * tex + 2];
@@ -966,7 +1042,15 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
     return o;
 }
 
-enum { PH_PIXEL = 0, PH_TRACE = 1, PH_SHADE = 2 };
+// PH_REF: the ray is traced on the reference tree (the SAH path's fallback, §5.6)
+enum { PH_PIXEL = 0, PH_TRACE = 1, PH_SHADE = 2, PH_REF = 3 };
+// traversal modes: the reference tree (DFS of hittable.rs:429-473 with hit_cond AND the cull), the
+// SAH tree (cull only, closest hit with ties flagged), the reference tree for PH_REF lanes with
+// the scene in HBM (the LDS holds the SAH tree)
+enum { TM_REF = 0, TM_SAH = 1, TM_FALLBACK = 2 };
+// Trav.fast bits above the direction signs (0-2) and the Markstein flag (3)
+#define RTW_TF_SAH 16  // the ray is traced on the SAH tree; te = the closest t's successor
+#define RTW_TF_TIE 32  // another leaf reported exactly the closest t
 
 // Experiment builds only (make variant DEFS=-DRTW_PHASE_TIMING): per-wave wall cycles of the main
 // loop's phases, summed over waves into rtw_phase_cycles (read by rtw_debug_phase_cycles).
@@ -987,7 +1071,8 @@ extern __shared__ __attribute__((aligned(16))) float4 smem[];
 struct Trav {
     Ray ray;
     V3 inv;         // RN(1 / ray.d)
-    int32_t fast;   // bits 0-2: ray.d[i] > 0 (the near child's side per axis); bit 3: Markstein division usable
+    int32_t fast;   // bits 0-2: ray.d[i] > 0 (the near child's side per axis); bit 3: Markstein division
+                    // usable; RTW_TF_SAH, RTW_TF_TIE
     int32_t node;   // current node (>= 0) or ~leaf
     int32_t sp;
     float te;       // t_range.end, shrunk by every hit (hittable.rs:457)
@@ -1002,14 +1087,6 @@ struct Trav {
 // The hot loop: every lane in PH_TRACE advances one node or leaf per iteration until fewer than
 // `trace_min` lanes are still tracing while some lane waits for shading (dynamic ray fetch).
 // Out of line so that it gets a register allocation of its own.
-// A plain-sphere leaf test with the current range; updates te/found on a hit.
-__device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, float& te, int32_t& found) {
-    float t;
-    if (sphere_t(sph, r, 0.001f, te, t)) {
-        te = t;
-        found = leaf;
-    }
-}
 
 // LDS modes of the render kernel: 0 scene in HBM, 1 nodes + leaf records + cull constants + rect
 // records in LDS, 2 also the plain-triangle records (tri_fast).  LDS layout: [node_a n][node_b n]
@@ -1021,28 +1098,51 @@ __device__ __forceinline__ void sphere_leaf(float4 sph, int leaf, const Ray& r, 
 // the RNG update alone made the compiler copy the lane's traversal registers at the leaf merge on
 // every leaf step.
 enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_WRAPPED = 3, LK_ANY = 4 };
-template <bool STATS, int LDS, int LK, bool FAST_ONLY>
+template <bool STATS, int LDS, int LK, bool FAST_ONLY, int TM = TM_REF>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
-                                      int32_t n_leaves, int32_t n_rects, int32_t n_tris, unsigned long long* dbg) {
-    constexpr bool LDS_SCENE = LDS >= 1;
+                                      int32_t n_leaves, int32_t n_rects, int32_t n_tris, int32_t stack_off,
+                                      unsigned long long* dbg) {
+    // the LDS holds the tree this mode walks (the SAH tree in SAH mode); the fallback reads HBM
+    constexpr bool LDS_SCENE = LDS >= 1 && TM != TM_FALLBACK;
+    constexpr int ACT = TM == TM_FALLBACK ? PH_REF : PH_TRACE;  // the lanes this loop advances
+    (void)n_tris;  // the stack offset comes from the caller
     const DWorld& w = *wp;
     // the plain-triangle records' base, loaded once per call into scalar registers (the world
     // struct is read through a pointer; left in the loop it becomes a dependent global load)
     const int32_t rect_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
     const int32_t tri_off = rect_off + 2 * n_rects;
     const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
-    const float4* tri_fast = LDS == 2 ? smem + tri_off : uniform_ptr(w.tri_fast);
+    const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
     // The LDS section offsets are held in VGPRs (opaque copies): as SGPRs they compete with the
     // loop's exec masks and get spilled to VGPR lanes, costing a v_readlane per node step.
     int32_t off_b = n_nodes, off_f = 2 * n_nodes, off_k = 2 * (2 * n_nodes + n_leaves);
     if (LDS_SCENE) asm volatile("" : "+v"(off_b), "+v"(off_f), "+v"(off_k));
-    const float4* nodes_a = LDS_SCENE ? smem : w.node_a;
-    const float4* nodes_b = LDS_SCENE ? smem + off_b : w.node_b;
+    const float4* nodes_a = LDS_SCENE ? smem : TM == TM_SAH ? w.sah_a : w.node_a;
+    const float4* nodes_b = LDS_SCENE ? smem + off_b : TM == TM_SAH ? w.sah_b : w.node_b;
     const float4* fast = LDS_SCENE ? smem + off_f : w.leaf_fast;
-    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem) + off_k : w.node_km;
-    int32_t* stack = reinterpret_cast<int32_t*>(smem + (LDS_SCENE ? tri_off + (LDS == 2 ? 4 * n_tris : 0) : 0)) +
-                     threadIdx.x;
+    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem) + off_k : TM == TM_SAH ? w.sah_km : w.node_km;
+    // 16-bit entries in LDS mode 2 (its triangle records cap the world far below 2^15 nodes and
+    // leaves): half the stack bytes, so that a deeper SAH tree still leaves room for the records
+    using StackEntry = std::conditional_t<LDS == 2, int16_t, int32_t>;
+    StackEntry* stack = reinterpret_cast<StackEntry*>(smem + stack_off) + threadIdx.x;
+    // a leaf's root t: the reference narrows te to it; the SAH walk keeps te = succ(closest t) so
+    // that a leaf reporting exactly the closest t again (a tie, whose winner is the reference's
+    // DFS order) is seen and flagged
+    auto take = [&](float t, int leaf) {
+        if (TM == TM_SAH) {
+            if (T.found >= 0 && t == __int_as_float(__float_as_int(T.te) - 1)) {
+                T.fast |= RTW_TF_TIE;
+            } else {
+                T.te = __int_as_float(__float_as_int(t) + 1);  // t >= 0.001: the next float up
+                T.found = leaf;
+                T.fast &= ~RTW_TF_TIE;
+            }
+        } else {
+            T.te = t;
+            T.found = leaf;
+        }
+    };
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
@@ -1057,13 +1157,15 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // one leaf body and one node body per iteration, both in the reference's DFS order with the
     // current t_range.  A lane reaching a leaf child tests it at the start of the next iteration.
     for (;;) {
-        const unsigned long long tr = __ballot(T.phase == PH_TRACE);
+        const unsigned long long tr = __ballot(T.phase == ACT);
         if (tr == 0) break;
         // dynamic ray fetch: leave for shading when fewer than trace_min lanes still trace and some
-        // lane waits (the threshold is tuned per world on the device, see TuneState)
-        if ((uint32_t)__popcll(tr) < (uint32_t)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
+        // lane waits (the threshold is tuned per world on the device, see TuneState); the fallback
+        // (rare lanes) runs to the end
+        if (TM != TM_FALLBACK && (uint32_t)__popcll(tr) < (uint32_t)trace_min && __ballot(T.phase == PH_SHADE) != 0)
+            break;
         if (STATS) {
-            const unsigned long long lm = __ballot(T.phase == PH_TRACE && T.node < 0);
+            const unsigned long long lm = __ballot(T.phase == ACT && T.node < 0);
             const uint32_t alive = (uint32_t)__popcll(__ballot(1));
             const uint32_t waiting = (uint32_t)__popcll(__ballot(T.phase == PH_SHADE));
             if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
@@ -1088,12 +1190,13 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         // often.  That pays where leaf steps are a small share (final_scene1 ~0.1 leaf per node
         // step, suzanne ~0.4: +3 %, +5 %) and costs where leaves come at every turn (cornell_cube's
         // wall rects, ~0.8: -8 %), hence only for worlds without rect, box or wrapped leaves.
-        if ((STATS || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == PH_TRACE && T.node < 0) {
+        if ((STATS || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
             const int leaf = -1 - T.node;
             const float4 sph = fast[leaf];
             if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
                 if (STATS) st.c[ST_T_SPHERE]++;
-                sphere_leaf(sph, leaf, T.ray, T.te, T.found);
+                float t;
+                if (sphere_t(sph, T.ray, 0.001f, T.te, t)) take(t, leaf);
             } else if (LK >= LK_PLAIN && __float_as_int(sph.x) == 2) {  // a plain rect
                 if (STATS) st.c[ST_T_RECT]++;
                 const int ri = __float_as_int(sph.y);
@@ -1101,40 +1204,32 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
                 float t;
                 V3 pos;
-                if (rect_t(g, T.ray, 0.001f, T.te, t, pos)) {
-                    T.te = t;
-                    T.found = leaf;
-                }
+                if (rect_t(g, T.ray, 0.001f, T.te, t, pos)) take(t, leaf);
             } else if (LK == LK_TRIS || LK == LK_PLAIN || __float_as_int(sph.x) == 1) {  // a plain triangle
                 if (STATS) st.c[ST_T_TRI]++;
                 float t;
-                if (tri_test(load_tri(tri_fast, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) {
-                    T.te = t;
-                    T.found = leaf;
-                }
+                if (tri_test(load_tri(tri_fast, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) take(t, leaf);
             } else if (LK >= LK_WRAPPED) {
                 float t;
-                if (leaf_t<STATS, LK == LK_ANY>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) {
-                    T.te = t;
-                    T.found = leaf;
-                }
+                if (leaf_t<STATS, LK == LK_ANY>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) take(t, leaf);
             }
             if (T.sp == 0) T.phase = PH_SHADE;
             else T.node = stack[(--T.sp) * RTW_BLOCK];
         }
         if (STATS) {
-            const unsigned long long nm = __ballot(T.phase == PH_TRACE && T.node >= 0);
+            const unsigned long long nm = __ballot(T.phase == ACT && T.node >= 0);
             if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
                 db[DB_NODE_ITERS] += nm != 0;
                 db[DB_NODE_LANES] += (uint32_t)__popcll(nm);
             }
         }
-        if (T.phase == PH_TRACE && T.node >= 0) {
+        if (T.phase == ACT && T.node >= 0) {
             if (STATS) st.c[ST_NODES]++;
             const float4 na = nodes_a[T.node];
             const float4 nb = nodes_b[T.node];
             const float2 km = nkm[T.node];
-            if (node_pass<FAST_ONLY>(na, nb, km, T.ray, rp, 0.001f, T.te)) {
+            if (TM == TM_SAH ? node_pass_cons(na, nb, km, T.ray, rp, 0.001f, T.te)
+                             : node_pass<FAST_ONLY>(na, nb, km, T.ray, rp, 0.001f, T.te)) {
                 if (STATS) db[DB_PASS_LANES]++;
                 const int32_t lbits = __float_as_int(nb.z);
                 const int32_t left = lbits >> 2;
@@ -1142,7 +1237,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 const int32_t right = __float_as_int(nb.w);
                 const bool fwd = __builtin_amdgcn_ubfe((uint32_t)T.fast, (uint32_t)axis, 1u) != 0u;  // ray.d[axis] > 0
                 // hit_index_list order: near subtree, then far
-                stack[(T.sp++) * RTW_BLOCK] = fwd ? right : left;
+                stack[(T.sp++) * RTW_BLOCK] = (StackEntry)(fwd ? right : left);
                 T.node = fwd ? left : right;
             } else if (T.sp == 0) {
                 T.phase = PH_SHADE;
@@ -1168,14 +1263,21 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
     // per node)] [stack: depth x BLOCK]
     const DWorld& w = A.w;
+    // SAH path (§5.6): worlds of plain spheres / triangles only, never in the counting variant
+    // (whose statistics are the reference traversal's)
+    constexpr bool SAHK = !STATS && LK <= LK_TRIS;
+    const bool sah = SAHK && A.sah != 0;
     if (LDS_SCENE) {
+        const float4* ga = sah ? w.sah_a : w.node_a;
+        const float4* gb = sah ? w.sah_b : w.node_b;
+        const float2* gk = sah ? w.sah_km : w.node_km;
         for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) {
-            smem[i] = w.node_a[i];
-            smem[A.node_count + i] = w.node_b[i];
+            smem[i] = ga[i];
+            smem[A.node_count + i] = gb[i];
         }
         for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
         float2* km = reinterpret_cast<float2*>(smem + 2 * A.node_count + A.leaf_count);
-        for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = w.node_km[i];
+        for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = gk[i];
         float4* rects = smem + 2 * A.node_count + A.leaf_count + (A.node_count + 1) / 2;
         for (int i = threadIdx.x; i < 2 * A.rect_count; i += RTW_BLOCK) rects[i] = w.rects[i];
         if (LDS == 2) {
@@ -1184,6 +1286,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
         __syncthreads();
     }
+    // the traversal stacks follow the LDS scene
+    const int32_t stack_off =
+        LDS_SCENE ? 2 * A.node_count + A.leaf_count + (A.node_count + 1) / 2 + 2 * A.rect_count + (LDS == 2 ? 4 * A.tri_count : 0)
+                  : 0;
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
@@ -1363,6 +1469,14 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             T.inv = rp.inv;
             T.fast = (rp.fast ? 8 : 0) | (T.ray.d.x > 0.0f ? 1 : 0) | (T.ray.d.y > 0.0f ? 2 : 0) | (T.ray.d.z > 0.0f ? 4 : 0);
             T.node = w.root;
+            if (sah) {  // the SAH walk needs the exact fast division; other rays take the reference tree
+                if (rp.fast) {
+                    T.node = w.sah_root;
+                    T.fast |= RTW_TF_SAH;
+                } else {
+                    T.phase = PH_REF;
+                }
+            }
             T.sp = 0;
             T.te = F32_INF;
             T.found = -1;
@@ -1373,14 +1487,49 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         RTW_PT(3);
         // (almost) every ray is Markstein-exact: such calls run a loop without the true-division
         // path (wave-uniform choice per call)
-        if (__ballot(T.phase == PH_TRACE && (T.fast & 8) == 0) == 0)
+        if (sah) {
+            T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
+                                                       A.leaf_count, A.rect_count, A.tri_count, stack_off, nullptr);
+            // §5.6: the SAH walk's closest leaf L (no tie) is the reference's answer when the
+            // reference DFS reaches L: every ancestor box contains L's Aabb (checked at upload) and
+            // hit_cond is monotone under box inclusion and in te, so L's own box passing hit_cond
+            // with te = succ(t) proves it.  A miss is a miss for the reference too.  Otherwise the
+            // ray is traced again on the reference tree.
+            if (T.phase == PH_SHADE && (T.fast & RTW_TF_SAH)) {
+                bool ok = (T.fast & RTW_TF_TIE) == 0;
+#ifdef RTW_SAH_AUDIT_NO_TIE  // audit builds only: shows that the tie test decides images
+                ok = true;
+#endif
+                if (T.found >= 0) {
+                    const float4 ba = w.leaf_box[2 * T.found], bb = w.leaf_box[2 * T.found + 1];
+#ifndef RTW_SAH_AUDIT_NO_BOX  // audit builds only: shows that the leaf-box proof decides images
+                    ok = ok && box_hit_cond_fast(ba, bb, T.ray, RayPre{T.inv, true}, 0.001f, T.te);
+#else
+                    (void)ba, (void)bb;
+#endif
+                    T.te = __int_as_float(__float_as_int(T.te) - 1);  // the closest t
+                }
+                T.fast &= ~(RTW_TF_SAH | RTW_TF_TIE);
+                if (!ok) {
+                    T.phase = PH_REF;
+                    T.node = w.root;
+                    T.sp = 0;
+                    T.te = F32_INF;
+                    T.found = -1;
+                }
+            }
+            if (__ballot(T.phase == PH_REF) != 0)
+                T = traverse<STATS, LDS, LK, false, TM_FALLBACK>(A.wdev, T, 0, A.node_count, A.leaf_count, A.rect_count,
+                                                                 A.tri_count, stack_off, nullptr);
+        } else if (__ballot(T.phase == PH_TRACE && (T.fast & 8) == 0) == 0) {
             T = traverse<STATS, LDS, LK, true>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
-                                               A.leaf_count, A.rect_count, A.tri_count,
+                                               A.leaf_count, A.rect_count, A.tri_count, stack_off,
                                                STATS ? A.stats + ST_COUNT : nullptr);
-        else
+        } else {
             T = traverse<STATS, LDS, LK, false>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
-                                                A.leaf_count, A.rect_count, A.tri_count,
+                                                A.leaf_count, A.rect_count, A.tri_count, stack_off,
                                                 STATS ? A.stats + ST_COUNT : nullptr);
+        }
         if (STATS) {
             c_mark = clock64();
             if (lane == __ffsll((long long)__ballot(1)) - 1)
@@ -1593,6 +1742,12 @@ __global__ void eval_scalar_kernel(int fn, const float* a, const float* b, int64
     out[i] = r;
 }
 
+__global__ void eval_checker_kernel(const float* xyz, int64_t n, int32_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = d_checker_odd(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]) ? 1 : 0;
+}
+
 __global__ void eval_node_pass_kernel(const float* box, const float* ray, const float* range, const float* km,
                                       int32_t mk_world, int64_t n, int32_t* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1734,6 +1889,85 @@ int check_world(const rtw_world* w, int* depth_out) {
     return RTW_OK;
 }
 
+// The SAH path's tables (§5.6), or empty when the world does not qualify: every leaf a plain
+// sphere or triangle, the reference tree's boxes nested (each child's box -- a leaf's own Aabb,
+// aabb.rs new_radius / new_surrounding_points -- inside its parent's), every leaf-box coordinate
+// admitting the exact fast division (0 or >= 2^-60 in magnitude), and RTW_NO_SAH unset.
+struct SahTables {
+    std::vector<float4> a, b;     // nodes, as node_a / node_b
+    std::vector<float> km;        // cull constants, 2 per node
+    std::vector<float4> box;      // 2 per leaf: the leaf's Aabb
+    int32_t root = 0, depth = 0;
+    bool ok = false;
+};
+SahTables build_sah_tables(const rtw_world* w) {
+    SahTables S;
+    if (const char* e = std::getenv("RTW_NO_SAH"))
+        if (e[0] && e[0] != '0') return S;
+    const int32_t L = w->leaf_count;
+    if (L < 2 || w->root < 0) return S;
+    std::vector<float> lo((size_t)L * 3), hi((size_t)L * 3);
+    for (int32_t i = 0; i < L; ++i) {
+        const rtw_leaf& l = w->leaves[i];
+        if (l.flags != 0) return S;
+        float* mn = &lo[3 * (size_t)i];
+        float* mx = &hi[3 * (size_t)i];
+        if (l.geom_kind == RTW_GEOM_SPHERE) {  // Aabb::new_radius: center -+ (r, r, r)
+            const rtw_sphere& sp = w->spheres[l.geom_index];
+            for (int k = 0; k < 3; ++k) {
+                mn[k] = sp.center[k] - sp.radius;
+                mx[k] = sp.center[k] + sp.radius;
+            }
+        } else if (l.geom_kind == RTW_GEOM_TRIANGLE) {  // Aabb::new_surrounding_points
+            const rtw_triangle& t = w->triangles[l.geom_index];
+            for (int k = 0; k < 3; ++k) {
+                mn[k] = rtw_minr(rtw_minr(t.positions[0][k], t.positions[1][k]), t.positions[2][k]);
+                mx[k] = rtw_maxr(rtw_maxr(t.positions[0][k], t.positions[1][k]), t.positions[2][k]);
+            }
+        } else {
+            return S;
+        }
+        for (int k = 0; k < 3; ++k)
+            for (float c : {mn[k], mx[k]})
+                if (!(c == 0.0f || (std::fabs(c) >= 0x1p-60f && std::fabs(c) <= 1073741824.0f))) return S;
+    }
+    // nested reference boxes: then every ancestor of a leaf contains the leaf's Aabb
+    for (int32_t n = 0; n < w->node_count; ++n) {
+        const rtw_bvh_node& nd = w->nodes[n];
+        for (int32_t c : {nd.left, nd.right}) {
+            const float* cmn = c >= 0 ? w->nodes[c].min : &lo[3 * (size_t)(-1 - c)];
+            const float* cmx = c >= 0 ? w->nodes[c].max : &hi[3 * (size_t)(-1 - c)];
+            for (int k = 0; k < 3; ++k)
+                if (!(nd.min[k] <= cmn[k] && cmx[k] <= nd.max[k])) return S;
+        }
+    }
+    std::vector<rtw_bvh_node> nodes;
+    if (rtw::sah_build(lo.data(), hi.data(), L, nodes, &S.root, &S.depth) != 0 || S.depth > RTW_STACK) return S;
+    // cull constants of the SAH tree: the same per-leaf bounds, maximised over its subtrees
+    rtw_world tw = *w;
+    tw.nodes = nodes.data();
+    tw.node_count = (int32_t)nodes.size();
+    tw.root = S.root;
+    S.km.assign(nodes.size() * 2, 0.0f);
+    rtw_cull_prepare(&tw, S.km.data(), 0);
+    S.a.resize(nodes.size());
+    S.b.resize(nodes.size());
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        const rtw_bvh_node& n = nodes[i];
+        S.a[i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
+        S.b[i] = make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
+    }
+    S.box.resize((size_t)L * 2);
+    for (int32_t i = 0; i < L; ++i) {
+        const float* mn = &lo[3 * (size_t)i];
+        const float* mx = &hi[3 * (size_t)i];
+        S.box[2 * (size_t)i] = make_float4(mn[0], mn[1], mn[2], mx[0]);
+        S.box[2 * (size_t)i + 1] = make_float4(mx[1], mx[2], 0.0f, 0.0f);
+    }
+    S.ok = true;
+    return S;
+}
+
 }  // namespace
 
 struct rtw_gpu_world {
@@ -1749,6 +1983,7 @@ struct rtw_gpu_world {
     int32_t node_count = 0, leaf_count = 0, depth = 1;
     int32_t tri_count = 0, rect_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
+    int32_t sah_nodes = 0;  // nodes of the SAH tree, 0: the world takes the reference tree only (§5.6)
     int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
     int32_t tex_kinds = TX_ANY;   // TX_*: the texture code the world's textures need
     int cus = 0;
@@ -1766,7 +2001,7 @@ struct rtw_gpu_world {
     bool done_recorded = false;
     uint32_t order_tiles = 0;
     bool order_valid = false;      // tile permutation computed for order_key
-    int32_t last_kernel[3] = {-1, -1, -1};  // LDS mode, leaf kinds, texture kinds of the last render
+    int32_t last_kernel[4] = {-1, -1, -1, -1};  // LDS mode, leaf kinds, texture kinds, tree of the last render
 };
 
 // experiment builds (-DRTW_PHASE_TIMING): read and reset the phase cycle sums
@@ -1930,6 +2165,11 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     const size_t o_pr = L.push(pr.data(), pr.size() * sizeof(float));
     const size_t o_pp = L.push(pp.data(), pp.size() * sizeof(uint32_t));
     const size_t o_pb = L.push(pb.data(), pb.size() * sizeof(int));
+    const SahTables sah = build_sah_tables(w);
+    const size_t o_sa = sah.ok ? L.push(sah.a.data(), sah.a.size() * sizeof(float4)) : 0;
+    const size_t o_sb = sah.ok ? L.push(sah.b.data(), sah.b.size() * sizeof(float4)) : 0;
+    const size_t o_sk = sah.ok ? L.push(sah.km.data(), sah.km.size() * sizeof(float)) : 0;
+    const size_t o_lb = sah.ok ? L.push(sah.box.data(), sah.box.size() * sizeof(float4)) : 0;
     WorldConst wcst;
     std::memset(&wcst, 0, sizeof(wcst));
     wcst.cam = w->camera;
@@ -1974,6 +2214,13 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     d.perlin_perm = (const uint32_t*)(base + o_pp);
     d.perlin_bits = (const int*)(base + o_pb);
     d.root = w->root;
+    if (sah.ok) {
+        d.sah_a = (const float4*)(base + o_sa);
+        d.sah_b = (const float4*)(base + o_sb);
+        d.sah_km = (const float2*)(base + o_sk);
+        d.leaf_box = (const float4*)(base + o_lb);
+        d.sah_root = sah.root;
+    }
     d.has_light = w->has_light;
     d.wc = (const WorldConst*)(base + o_wc);
     e = hipMemcpy(base + o_dw, &g->w, sizeof(DWorld), hipMemcpyHostToDevice);
@@ -1986,6 +2233,10 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->node_count = w->node_count;
     g->leaf_count = w->leaf_count;
     g->depth = std::max(1, depth);
+    if (sah.ok) {
+        g->sah_nodes = (int32_t)sah.a.size();
+        g->depth = std::max(g->depth, sah.depth);
+    }
     g->tri_count = w->triangle_count;
     g->rect_count = w->rect_count;
     g->mk_world = 1;
@@ -2040,11 +2291,12 @@ extern "C" RTW_API int rtw_world_tuning(rtw_gpu_world* g, int* trace_min) {
     return RTW_OK;
 }
 
-extern "C" RTW_API int rtw_world_kernel(rtw_gpu_world* g, int* lds_mode, int* leaf_kinds, int* tex_kinds) {
-    if (!g || !lds_mode || !leaf_kinds || !tex_kinds) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+extern "C" RTW_API int rtw_world_kernel(rtw_gpu_world* g, int* lds_mode, int* leaf_kinds, int* tex_kinds, int* tree) {
+    if (!g || !lds_mode || !leaf_kinds || !tex_kinds || !tree) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
     *lds_mode = g->last_kernel[0];
     *leaf_kinds = g->last_kernel[1];
     *tex_kinds = g->last_kernel[2];
+    *tree = g->last_kernel[3];
     return RTW_OK;
 }
 
@@ -2120,19 +2372,31 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
 enum LaunchKind { LK_RENDER, LK_STATS };
 int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const bool stats = kind == LK_STATS;
+    // the leaf and texture kinds the world needs; RTW_LEAF_KINDS=4 / RTW_TEX_KINDS=1 force the
+    // generic code (audits)
+    int lk = g->leaf_kinds, tx = g->tex_kinds;
+    if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(4, std::atoi(e)));
+    if (const char* e = std::getenv("RTW_TEX_KINDS")) tx = std::max(tx, std::min(1, std::atoi(e)));
+    // the SAH tree (§5.6) replaces the reference tree in LDS; the counting variant keeps the latter
+    const bool sah = !stats && g->sah_nodes > 0 && g->mk_world && lk <= LK_TRIS;
+    A.sah = sah ? 1 : 0;
+    A.node_count = sah ? g->sah_nodes : g->node_count;
     const size_t scene_bytes =
-        (size_t)(2 * g->node_count + g->leaf_count + (g->node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
+        (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
     const size_t tri_bytes = (size_t)g->tri_count * 4 * sizeof(float4);
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
+    const size_t stack16_bytes = stack_bytes / 2;  // mode 2: 16-bit entries
     // a block may take its share of the CU's LDS at the kernel's target occupancy
     // (RTW_MIN_WAVES_PER_SIMD waves on each of 4 SIMDs)
     const int blocks_per_cu = std::max(1, (4 * RTW_MIN_WAVES_PER_SIMD * 64) / RTW_BLOCK);
     const size_t cap = std::min({(size_t)RTW_LDS_SCENE_MAX, (size_t)g->lds_max, (size_t)g->lds_cu / blocks_per_cu});
     int mode = 0;
-    if (g->tri_count > 0 && scene_bytes + tri_bytes + stack_bytes <= cap) mode = 2;
+    if (g->tri_count > 0 && g->leaf_count < 32768 && A.node_count < 32768 && g->node_count < 32768 &&
+        scene_bytes + tri_bytes + stack16_bytes <= cap)
+        mode = 2;
     else if (scene_bytes + stack_bytes <= cap) mode = 1;
     if (const char* e = std::getenv("RTW_LDS_MODE")) mode = std::min(mode, std::atoi(e));  // audits: cap the mode
-    const size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes : 0) + stack_bytes;
+    const size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes + stack16_bytes : stack_bytes);
     using KFn = void (*)(KArgs);
 #define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}
     static const KFn fns[2][5][3] = {
@@ -2143,16 +2407,12 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
 #undef RTW_KSET
     static const KFn fns_stats[3] = {render_kernel<true, 0, LK_ANY, TX_ANY>, render_kernel<true, 1, LK_ANY, TX_ANY>,
                                      render_kernel<true, 2, LK_ANY, TX_ANY>};
-    // the leaf and texture kinds the world needs; RTW_LEAF_KINDS=4 / RTW_TEX_KINDS=1 force the
-    // generic code (audits)
-    int lk = g->leaf_kinds, tx = g->tex_kinds;
-    if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(4, std::atoi(e)));
-    if (const char* e = std::getenv("RTW_TEX_KINDS")) tx = std::max(tx, std::min(1, std::atoi(e)));
     const KFn kf = stats ? fns_stats[mode] : fns[tx][lk][mode];
     if (!stats) {
         g->last_kernel[0] = mode;
         g->last_kernel[1] = lk;
         g->last_kernel[2] = tx;
+        g->last_kernel[3] = sah ? 1 : 0;
     }
     const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2591,6 +2851,25 @@ extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, c
     (void)hipFree(dr);
     (void)hipFree(dg);
     (void)hipFree(dk);
+    (void)hipFree(dout);
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_device_eval_checker(int device, const float* xyz, int64_t n, int32_t* out) {
+    if (!xyz || !out || n < 0) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device");
+    HIP_TRY(hipSetDevice(device));
+    if (n == 0) return RTW_OK;
+    float* dx = nullptr;
+    int32_t* dout = nullptr;
+    HIP_TRY(hipMalloc(&dx, (size_t)n * 3 * sizeof(float)));
+    HIP_TRY(hipMalloc(&dout, (size_t)n * sizeof(int32_t)));
+    HIP_TRY(hipMemcpy(dx, xyz, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(eval_checker_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, n, dout);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(out, dout, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    (void)hipFree(dx);
     (void)hipFree(dout);
     return RTW_OK;
 }

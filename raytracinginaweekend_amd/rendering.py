@@ -126,10 +126,11 @@ class DeviceWorld:
         return v.value
 
     def kernel_variant(self) -> dict:
-        """The render-kernel variant of the last render (LDS mode, leaf kinds, texture kinds)."""
-        m, lk, tx = C.c_int(), C.c_int(), C.c_int()
-        check(lib().rtw_world_kernel(self._h, C.byref(m), C.byref(lk), C.byref(tx)))
-        return {"lds_mode": m.value, "leaf_kinds": lk.value, "tex_kinds": tx.value}
+        """The render-kernel variant of the last render (LDS mode, leaf kinds, texture kinds, tree)."""
+        m, lk, tx, tr = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        check(lib().rtw_world_kernel(self._h, C.byref(m), C.byref(lk), C.byref(tx), C.byref(tr)))
+        return {"lds_mode": m.value, "leaf_kinds": lk.value, "tex_kinds": tx.value,
+                "tree": ("reference", "sah")[tr.value] if tr.value >= 0 else None}
 
     def collect_stats(self, params: N.RenderParams) -> dict:
         s = N.RenderStats()

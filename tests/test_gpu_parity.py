@@ -137,18 +137,70 @@ def test_true_division_loop_agrees(worlds, name, monkeypatch):
     assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(40, 24), 4, 50, seed=23)), name)
 
 
+def _kernel_tree(world) -> str:
+    import torch
+
+    dw = R.DeviceWorld(world, 0)
+    out = torch.empty(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
+    dw.render_into(R.render_params(R.Size2i(16, 16), 1, 50), out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    return dw.kernel_variant()["tree"]
+
+
 @pytest.mark.parametrize("name", ["final_scene1", "suzanne"])
-def test_true_division_loop_agrees(worlds, name, monkeypatch):
-    """Every ray on the true-division slab test (the general traversal loop, RTW_NO_MARKSTEIN=1)
-    gives the Markstein loop's bits on a GPU-filling frame, and the oracle's on a small one."""
+def test_sah_tree_agrees(worlds, name, monkeypatch):
+    """closest hits found on the kernel's SAH tree (verified against the reference
+    tree's order, re-traced there where the proof fails) give the reference-tree loop's bits
+    (RTW_NO_SAH=1) on a GPU-filling frame, and the oracle's on a small one."""
     world = worlds(name)
+    assert _kernel_tree(world) == "sah"
     size = R.Size2i(320, 180)
-    fast = R.render(size, 1, 8, 50, world, seed=23)
-    monkeypatch.setenv("RTW_NO_MARKSTEIN", "1")
-    slow = R.render(size, 1, 8, 50, world, seed=23)
-    small = R.render(R.Size2i(40, 24), 1, 4, 50, world, seed=23)
-    assert_bit_identical(fast, slow, name + " Markstein vs true-division loop")
-    assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(40, 24), 4, 50, seed=23)), name)
+    sah = R.render(size, 1, 8, 50, world, seed=29)
+    small = R.render(R.Size2i(40, 24), 1, 4, 50, world, seed=29)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert _kernel_tree(world) == "reference"
+    ref = R.render(size, 1, 8, 50, world, seed=29)
+    assert_bit_identical(sah, ref, name + " SAH vs reference tree")
+    assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(40, 24), 4, 50, seed=29)), name)
+
+
+def _tie_world():
+    """Exact ties and grazing hits: four coincident spheres with different materials (every hit on
+    them is a tie the reference breaks by its DFS order), a row of touching spheres (tangent
+    points on shared box planes), and a quad of two triangles twice over (coincident triangles,
+    a shared diagonal)."""
+    wb = R.WorldBuilder()
+    mats = [wb.material_lambert_solid((0.8, 0.2, 0.2)), wb.material_lambert_solid((0.2, 0.8, 0.2)),
+            wb.material_metal_solid((0.7, 0.7, 0.7), 0.1), wb.material_dielectric(1.5)]
+    g = wb.new_group()
+    g.add(wb.new_obj_sphere(100.0, mats[0]).translate((0.0, -100.0, 0.0)))
+    for i in range(4):
+        g.add(wb.new_obj_sphere(0.5, mats[i]).translate((0.0, 0.5, 0.0)))
+    for k in range(7):
+        g.add(wb.new_obj_sphere(0.25, mats[k % 3]).translate((-1.5 + 0.5 * k, 0.25, 1.0)))
+    p = [(-2.0, 0.0, -1.0), (2.0, 0.0, -1.0), (2.0, 2.0, -1.0), (-2.0, 2.0, -1.0)]
+    n = (0.0, 0.0, 1.0)
+
+    def tri(a, b, c):
+        return list(p[a]) + list(p[b]) + list(p[c]) + list(n) * 3 + [0.0] * 6
+
+    quad = np.array([tri(0, 1, 2), tri(0, 2, 3)], np.float32)
+    g.add(wb.new_mesh(quad, mats[1]))
+    g.add(wb.new_mesh(quad, mats[2]))
+    cam = R.Camera.build().vertical_fov(40.0, 9.0 / 16.0).position((0.3, 1.2, 5.0)).look_at((0, 1, 0), (0, 0.5, 0)).build()
+    return g.build().finish(wb, R.BackgroundColor.sky(), cam)
+
+
+def test_sah_ties_and_grazing_hits(monkeypatch):
+    world = _tie_world()
+    assert _kernel_tree(world) == "sah"
+    size = R.Size2i(96, 54)
+    gpu = R.render(size, 1, 8, 50, world, seed=31)
+    assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=31)), "tie world")
+    big = R.Size2i(480, 270)
+    sah = R.render(big, 1, 4, 50, world, seed=31)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert_bit_identical(sah, R.render(big, 1, 4, 50, world, seed=31), "tie world, SAH vs reference tree")
 
 
 def test_progress_callback_reports_and_keeps_bits(worlds):

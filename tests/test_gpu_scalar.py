@@ -49,3 +49,36 @@ def test_binary(fn, name):
     a = np.concatenate([a, np.repeat(sp, len(sp))])
     b = np.concatenate([b, np.tile(sp, len(sp))])
     assert_bit_identical(_device(fn, a, b), O.eval_scalar(fn, a, b), name)
+
+
+def test_checker_sign():
+    """CheckerTexture's `sines < 0` (texture.rs:33-40): the kernel decides it from rtw_sinf's
+    quadrant reduction when that is unambiguous, else from the sines; the oracle multiplies the
+    f32 sines (RN at each product)."""
+    rng = np.random.default_rng(77)
+    n = 600_000
+    parts = [
+        rng.uniform(-2000, 2000, (n, 3)).astype(np.float32),                  # pos * 10 on the ground sphere
+        rng.uniform(-4, 4, (n, 3)).astype(np.float32),
+        _random_floats(rng, 3 * n).reshape(n, 3),
+    ]
+    # floats next to multiples of pi/2 (small remainders), tiny / zero / subnormal / huge / non-finite
+    k = np.arange(-400_000, 400_000, 7, dtype=np.float64)
+    near = (k * (np.pi / 2)).astype(np.float32)
+    near = np.concatenate([near, np.nextafter(near, np.float32(np.inf)), np.nextafter(near, np.float32(-np.inf))])
+    m = len(near)
+    parts.append(np.stack([near, rng.permutation(near), rng.uniform(-3, 3, m).astype(np.float32)], 1))
+    sp = np.array([0.0, -0.0, 1e-45, -1e-45, 1e-38, -3e-39, 2.0**-31, -(2.0**-30), 2.0**-29, 1e-20, -1e-30,
+                   2.0**19, -(2.0**19), 2.0**19 - 0.03125, 3.4e38, np.inf, -np.inf, np.nan, 1.0, -1.0, 3.1415927,
+                   -3.1415927, 1.5707964], np.float32)
+    g = np.stack(np.meshgrid(sp, sp, sp, indexing="ij"), -1).reshape(-1, 3)
+    parts.append(g)
+    xyz = np.ascontiguousarray(np.concatenate(parts).astype(np.float32))
+    out = np.empty(len(xyz), np.int32)
+    N.check(N.lib().rtw_device_eval_checker(0, xyz.ctypes.data_as(C.POINTER(C.c_float)), len(xyz),
+                                            out.ctypes.data_as(C.POINTER(C.c_int32))))
+    s = O.eval_scalar(3, xyz.reshape(-1)).reshape(-1, 3)
+    with np.errstate(all="ignore"):
+        want = ((s[:, 0] * s[:, 1]) * s[:, 2] < np.float32(0)).astype(np.int32)
+    bad = np.nonzero(out != want)[0]
+    assert len(bad) == 0, f"{len(bad)} mismatches, first {xyz[bad[:5]]}"
