@@ -266,7 +266,7 @@ RTW_API int rtw_world_tuning(rtw_gpu_world* gw, int* trace_min);
 /* The render-kernel variant this world's last render launched: LDS mode (0 scene in HBM, 1 tree +
  * leaf records in LDS, 2 + triangle records), leaf kinds (0 plain spheres .. 4 any), texture
  * kinds (0 solid only, 1 any) and search tree (0 the reference BVH, 1 the kernel's SAH tree with
- * the reference-order proof and fallback, DESIGN.md 5.6); -1 each before the first render.
+ * the reference-order proof and fallback, DESIGN.md 5.5); -1 each before the first render.
  * Diagnostics only. */
 RTW_API int rtw_world_kernel(rtw_gpu_world* gw, int* lds_mode, int* leaf_kinds, int* tex_kinds, int* tree);
 /* Renders this partition's tiles into device buffer `d_out` (layout per params->layout) on

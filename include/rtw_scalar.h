@@ -478,16 +478,25 @@ RTW_HD float rtw_sinf(float x) {
 /* would accept a root in [ts, te), so the closest hit, its tie-breaking and every RNG draw     */
 /* are those of the reference traversal (argument and error bounds: DESIGN.md "Proximity       */
 /* cull"; node constants k, m: rtw_cull.h).                                                     */
-/*   per (ray, node): D = sum_i (|min_i - o_i| + |max_i - o_i|) >= |o - x| for every x in     */
-/*   the box; delta = k D^2 + 64u D + m bounds how far outside the box a computed hit point of  */
+/*   per (ray, node): Dq = sum_i max(|min_i - o_i|, |max_i - o_i|)^2 >= |o - x|^2 for every x  */
+/*   in the box, D = sum of the same maxima >= |o - x|; delta = k Dq + 64u D + m bounds how far   */
+/*   outside the box a computed hit point of                                                     */
 /*   a leaf below can lie (plus the quotient roundings); the node passes when the ray segment   */
 /*   [ts, te] meets the box grown by delta, reusing hit_cond's slab quotients.                  */
 /* ------------------------------------------------------------------------------------------ */
 #define RTW_CULL_U 0x1p-24f
-/* (k D + 64u) D + m, two fused steps (host and device round identically; any rounding of this
- * bound is far inside the 9x safety factor of the cull analysis) */
-RTW_HD float rtw_cull_delta(float k, float m, float d) {
-    return __builtin_fmaf(__builtin_fmaf(k, d, 64.0f * RTW_CULL_U), d, m);
+/* delta = k Dq + 64u D + m for a node box and a ray origin, with a_i = min_i - o_i,
+ * b_i = max_i - o_i, M_i = max(|a_i|, |b_i|) (the farthest corner's offsets), Dq = sum_i M_i^2 and
+ * D = sum_i M_i: for every x in the box |o - x|^2 <= Dq and |o - x| <= D, which is all the bound
+ * uses of them.  Fused steps: host and device round identically (any rounding of this bound is far
+ * inside the safety factor of the cull analysis). */
+RTW_HD float rtw_cull_delta(float k, float m, float a0, float b0, float a1, float b1, float a2, float b2) {
+    const float m0 = __builtin_fmaxf(__builtin_fabsf(a0), __builtin_fabsf(b0));
+    const float m1 = __builtin_fmaxf(__builtin_fabsf(a1), __builtin_fabsf(b1));
+    const float m2 = __builtin_fmaxf(__builtin_fabsf(a2), __builtin_fabsf(b2));
+    const float d = (m0 + m1) + m2;
+    const float dq = __builtin_fmaf(m2, m2, __builtin_fmaf(m1, m1, m0 * m0));
+    return __builtin_fmaf(k, dq, __builtin_fmaf(64.0f * RTW_CULL_U, d, m));
 }
 /* one axis: [t0 - w, t1 + w] narrows [lo, hi]; NaN operands are dropped (conservative) */
 RTW_HD void rtw_cull_axis(float t0, float t1, float w, float* lo, float* hi) {

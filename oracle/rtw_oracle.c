@@ -377,16 +377,17 @@ static int aabb_hit_cond(const rtw_bvh_node* nd, const Ray* r, float ts, float t
  * RTW_ORACLE_CULL mode applies it after hit_cond to check, on the CPU, that it changes no
  * result and to count the culled traversal's work. */
 static int cull_pass(const float* km, int32_t n, const rtw_bvh_node* nd, const Ray* r, float ts, float te) {
-    float d = 0.0f, t0[3], t1[3];
+    float ab[6], t0[3], t1[3];
     for (int i = 0; i < 3; ++i) {
         const float a = nd->min[i] - r->origin.e[i];
         const float b = nd->max[i] - r->origin.e[i];
-        d += fabsf(a) + fabsf(b);
+        ab[2 * i] = a;
+        ab[2 * i + 1] = b;
         const float qa = a / r->dir.e[i], qb = b / r->dir.e[i];
         t0[i] = (qa < qb) ? qa : qb;
         t1[i] = (qa < qb) ? qb : qa;
     }
-    const float delta = rtw_cull_delta(km[2 * (size_t)n], km[2 * (size_t)n + 1], d);
+    const float delta = rtw_cull_delta(km[2 * (size_t)n], km[2 * (size_t)n + 1], ab[0], ab[1], ab[2], ab[3], ab[4], ab[5]);
     float lo = ts, hi = te;
     for (int i = 0; i < 3; ++i) rtw_cull_axis(t0[i], t1[i], delta * fabsf(1.0f / r->dir.e[i]), &lo, &hi);
     return lo <= hi;

@@ -662,10 +662,7 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
     const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
-    // D = sum_i |a_i| + |b_i| (>= sum_i max(|a_i|, |b_i|) >= |o - x|; abs-modifier adds, no max)
-    const float dsum = ((__builtin_fabsf(a0) + __builtin_fabsf(b0)) + (__builtin_fabsf(a1) + __builtin_fabsf(b1))) +
-                       (__builtin_fabsf(a2) + __builtin_fabsf(b2));
-    const float delta = rtw_cull_delta(km.x, km.y, dsum);
+    const float delta = rtw_cull_delta(km.x, km.y, a0, b0, a1, b1, a2, b2);
     if (FAST_ONLY || __builtin_expect(rp.fast, 1)) {
         const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
         const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
@@ -726,9 +723,7 @@ __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, 
     const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
-    const float dsum = ((__builtin_fabsf(a0) + __builtin_fabsf(b0)) + (__builtin_fabsf(a1) + __builtin_fabsf(b1))) +
-                       (__builtin_fabsf(a2) + __builtin_fabsf(b2));
-    const float delta = rtw_cull_delta(km.x, km.y, dsum);
+    const float delta = rtw_cull_delta(km.x, km.y, a0, b0, a1, b1, a2, b2);
     const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
     const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
     const float qa2 = mk_div(a2, r.d.z, rp.inv.z), qb2 = mk_div(b2, r.d.z, rp.inv.z);

@@ -5,7 +5,7 @@
 // ray enters.  The kernel answers "which leaf is closest" on a surface-area-heuristic tree built
 // here, visited with the proximity cull alone (conservative: never skips a leaf whose test would
 // accept a root in [ts, te)), and proves the answer is the reference's with one slab test on the
-// found leaf's own box (DESIGN.md §5.6).  The tree's shape affects speed only.
+// found leaf's own box (DESIGN.md §5.5).  The tree's shape affects speed only.
 #include <algorithm>
 #include <cmath>
 #include <vector>

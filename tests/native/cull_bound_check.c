@@ -66,15 +66,16 @@ static int tri_hit(const V* p, V o, V d, float ts, float te, float* t) {
 
 /* the cull predicate exactly as the oracle / kernel evaluate it (node box = lo, hi) */
 static int cull_pass(const float lo[3], const float hi[3], float k, float m, V o, V d, float ts, float te) {
-    float D = 0.0f, t0[3], t1[3];
+    float ab[6], t0[3], t1[3];
     for (int i = 0; i < 3; ++i) {
         const float a = lo[i] - o.e[i], b = hi[i] - o.e[i];
-        D += fabsf(a) + fabsf(b);
+        ab[2 * i] = a;
+        ab[2 * i + 1] = b;
         const float qa = a / d.e[i], qb = b / d.e[i];
         t0[i] = (qa < qb) ? qa : qb;
         t1[i] = (qa < qb) ? qb : qa;
     }
-    const float delta = rtw_cull_delta(k, m, D);
+    const float delta = rtw_cull_delta(k, m, ab[0], ab[1], ab[2], ab[3], ab[4], ab[5]);
     float l = ts, h = te;
     for (int i = 0; i < 3; ++i) rtw_cull_axis(t0[i], t1[i], delta * fabsf(1.0f / d.e[i]), &l, &h);
     return l <= h;
@@ -90,9 +91,13 @@ static double outside(const float lo[3], const float hi[3], V o, V d, float t) {
     return m;
 }
 static double delta_of(const float lo[3], const float hi[3], float k, float m, V o) {
-    double D = 0.0;
-    for (int i = 0; i < 3; ++i) D += fabs((double)lo[i] - o.e[i]) + fabs((double)hi[i] - o.e[i]);
-    return (double)k * D * D + 64.0 * 0x1p-24 * D + (double)m;
+    double D = 0.0, Dq = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        const double mi = fmax(fabs((double)lo[i] - o.e[i]), fabs((double)hi[i] - o.e[i]));
+        D += mi;
+        Dq += mi * mi;
+    }
+    return (double)k * Dq + 64.0 * 0x1p-24 * D + (double)m;
 }
 
 static V rnd_dir(void) {

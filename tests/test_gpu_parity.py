@@ -149,7 +149,7 @@ def _kernel_tree(world) -> str:
 
 @pytest.mark.parametrize("name", ["final_scene1", "suzanne"])
 def test_sah_tree_agrees(worlds, name, monkeypatch):
-    """DESIGN 5.6: closest hits found on the kernel's SAH tree (verified against the reference
+    """DESIGN 5.5: closest hits found on the kernel's SAH tree (verified against the reference
     tree's order, re-traced there where the proof fails) give the reference-tree loop's bits
     (RTW_NO_SAH=1) on a GPU-filling frame, and the oracle's on a small one."""
     world = worlds(name)
