@@ -1037,6 +1037,11 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
     return o;
 }
 
+#ifdef RTW_WAVE_TIMING  // experiment builds: per-wave start / end / queue-empty wall clocks of the last launch
+__device__ unsigned long long rtw_wave_times[3 * 8192];
+__device__ unsigned long long rtw_wave_dry[8192];  // first time a lane of the wave found the queue empty
+#endif
+
 // PH_REF: the ray is traced on the reference tree (the SAH path's fallback, §5.6)
 enum { PH_PIXEL = 0, PH_TRACE = 1, PH_SHADE = 2, PH_REF = 3 };
 // traversal modes: the reference tree (DFS of hittable.rs:429-473 with hit_cond AND the cull), the
@@ -1412,6 +1417,12 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 const uint64_t r = (uint64_t)__popcll(below);
                 const uint64_t item = r < left ? first + r : base + (r - left);
                 if (item >= A.items) {
+#ifdef RTW_WAVE_TIMING
+                    {
+                        const uint32_t wv_ = (blockIdx.x * RTW_BLOCK + threadIdx.x) / 64;
+                        if (wv_ < 8192) atomicMin(&rtw_wave_dry[wv_], (unsigned long long)wall_clock64());
+                    }
+#endif
                     out_of_work = true;
                     T.phase = PH_TRACE;  // leaves the loops below
                 } else {
@@ -1593,7 +1604,19 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 
 template <bool STATS, int LDS, int LK, int TX>
 __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
+#ifdef RTW_WAVE_TIMING
+    const uint64_t t_start = wall_clock64();
+#endif
     render_body<STATS, LDS, LK, TX>(A);
+#ifdef RTW_WAVE_TIMING
+    const uint32_t wv = (blockIdx.x * RTW_BLOCK + threadIdx.x) / 64;
+    if ((threadIdx.x & 63) == 0 && wv < 8192) {
+        rtw_wave_times[3 * wv] = t_start;
+        rtw_wave_times[3 * wv + 1] = wall_clock64();
+        rtw_wave_times[3 * wv + 2] = rtw_wave_dry[wv];
+        rtw_wave_dry[wv] = ~0ull;
+    }
+#endif
 }
 // Per slot: sum += colour of each sample of this launch, in sample order (the running sum of
 // earlier launches is carried in `running`); the last launch writes sum / spp (rendering.rs:179;
@@ -1998,6 +2021,19 @@ struct rtw_gpu_world {
     bool order_valid = false;      // tile permutation computed for order_key
     int32_t last_kernel[4] = {-1, -1, -1, -1};  // LDS mode, leaf kinds, texture kinds, tree of the last render
 };
+
+// experiment builds (-DRTW_WAVE_TIMING): per-wave start / end / queue-empty wall clocks (100 MHz) of
+// the last launch (tools/wave_timing.py; the first launch's queue-empty stamps are not valid)
+extern "C" RTW_API int rtw_debug_wave_times(unsigned long long* out24576) {
+#ifdef RTW_WAVE_TIMING
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out24576, HIP_SYMBOL(rtw_wave_times), 3 * 8192 * sizeof(unsigned long long)));
+    return RTW_OK;
+#else
+    (void)out24576;
+    return rtw::fail(RTW_ERR_UNSUPPORTED, "built without RTW_WAVE_TIMING");
+#endif
+}
 
 // experiment builds (-DRTW_PHASE_TIMING): read and reset the phase cycle sums
 extern "C" RTW_API int rtw_debug_phase_cycles(unsigned long long* out8) {

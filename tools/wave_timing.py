@@ -53,17 +53,6 @@ def main():
           f"ends (ms) min {q[0]:.2f} p10 {q[1]:.2f} p50 {q[2]:.2f} p90 {q[3]:.2f} p99 {q[4]:.2f} max {q[5]:.2f}; "
           f"queue empty (ms) min {qd[0]:.2f} p50 {qd[1]:.2f} max {qd[2]:.2f}; drain after it p50 {dr[0]:.2f} p90 {dr[1]:.2f} "
           f"p99 {dr[2]:.2f} max {dr[3]:.2f}")
-    lf = os.environ.get("RTW_WAVE_LATE_OUT")
-    if lf and os.path.exists(lf):
-        raw = np.fromfile(lf, np.uint32)
-        keep = buf.reshape(-1, 3)[:, 1] > 0
-        late = raw[: 2 * 8192].reshape(-1, 2)[keep]
-        rounds = raw[2 * 8192:].reshape(-1, 2)[keep]
-        slow = np.argsort(en - dry)[-10:]
-        for i in slow:
-            print(f"  wave drain {en[i] - dry[i]:.2f} ms: {late[i, 0]} samples after empty, max bounces {late[i, 1]}, "
-                  f"{rounds[i, 0]} main-loop rounds, deep late pixel (x, y) = ({rounds[i, 1] % a.width}, {rounds[i, 1] // a.width})")
-        print(f"  all waves: late samples mean {late[:, 0].mean():.1f}, max bounces p50 {np.median(late[:, 1])}")
 
 
 if __name__ == "__main__":
