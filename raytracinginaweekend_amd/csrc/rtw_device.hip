@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -718,15 +720,37 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
 // meets the box grown by delta.  Conservative: never rejects a node below which a leaf's test
 // would accept a root in [ts, te) (§5.2), whatever the tree.  A NaN delta (k = inf, D = 0) drops
 // out of the bounds, as in rtw_cull_axis.
+// Cheap quotients: q = RN(a * RN(1/d)) is within 2.0001u |a/d| of a/d, where the exact-quotient
+// test (the reference tree's node_pass) uses RN(a/d), within u |a/d|.  Since delta >= 64u D and
+// D >= |a_i|, that error is <= w_i / 32 (w_i = delta / |d_i|), the two quotient roundings together
+// <= 3 w_i / 64.  The SAH tree's k and m are uploaded x17/16 rounded up and the D term is 68u
+// (sah_delta), so w_i here >= (17/16)(1 - 4u) w_i of the exact test: each bound of this interval
+// lies outside the exact test's bound (RN is monotone), and this test passes every node that
+// test passes.  One multiply per quotient instead of three operations.
+#define RTW_SAH_WIDEN (17.0f / 16.0f)
+__device__ __forceinline__ float sah_delta(float k, float m, float a0, float b0, float a1, float b1, float a2, float b2) {
+    const float m0 = __builtin_fmaxf(__builtin_fabsf(a0), __builtin_fabsf(b0));
+    const float m1 = __builtin_fmaxf(__builtin_fabsf(a1), __builtin_fabsf(b1));
+    const float m2 = __builtin_fmaxf(__builtin_fabsf(a2), __builtin_fabsf(b2));
+    const float d = (m0 + m1) + m2;
+    const float dq = __builtin_fmaf(m2, m2, __builtin_fmaf(m1, m1, m0 * m0));
+    return __builtin_fmaf(k, dq, __builtin_fmaf(64.0f * RTW_SAH_WIDEN * RTW_CULL_U, d, m));
+}
 __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, const Ray& r, const RayPre& rp, float ts,
                                                float te) {
     const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
-    const float delta = rtw_cull_delta(km.x, km.y, a0, b0, a1, b1, a2, b2);
+    const float delta = sah_delta(km.x, km.y, a0, b0, a1, b1, a2, b2);
+#ifdef RTW_SAH_EXACT_Q  // audit / A/B builds: the exact quotients of the reference tree's test
     const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
     const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
     const float qa2 = mk_div(a2, r.d.z, rp.inv.z), qb2 = mk_div(b2, r.d.z, rp.inv.z);
+#else
+    const float qa0 = a0 * rp.inv.x, qb0 = b0 * rp.inv.x;
+    const float qa1 = a1 * rp.inv.y, qb1 = b1 * rp.inv.y;
+    const float qa2 = a2 * rp.inv.z, qb2 = b2 * rp.inv.z;
+#endif
     const float w0 = delta * __builtin_fabsf(rp.inv.x), w1 = delta * __builtin_fabsf(rp.inv.y),
                 w2 = delta * __builtin_fabsf(rp.inv.z);
     const float lo = __builtin_fmaxf(
@@ -1968,6 +1992,8 @@ SahTables build_sah_tables(const rtw_world* w) {
     tw.root = S.root;
     S.km.assign(nodes.size() * 2, 0.0f);
     rtw_cull_prepare(&tw, S.km.data(), 0);
+    for (float& c : S.km)  // x17/16 rounded up (inf stays inf): the cheap quotients' slack, node_pass_cons
+        if (c > 0.0f) c = std::nextafter(c * RTW_SAH_WIDEN, std::numeric_limits<float>::infinity());
     S.a.resize(nodes.size());
     S.b.resize(nodes.size());
     for (size_t i = 0; i < nodes.size(); ++i) {
