@@ -737,7 +737,7 @@ __device__ __forceinline__ float sah_delta(float k, float m, float a0, float b0,
     return __builtin_fmaf(k, dq, __builtin_fmaf(64.0f * RTW_SAH_WIDEN * RTW_CULL_U, d, m));
 }
 __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, const Ray& r, const RayPre& rp, float ts,
-                                               float te) {
+                                               float te, float& entry) {
     const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
@@ -761,6 +761,7 @@ __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, 
         __builtin_fminf(__builtin_fminf(__builtin_fmaxf(qa0, qb0) + w0, __builtin_fmaxf(qa1, qb1) + w1),
                         __builtin_fmaxf(qa2, qb2) + w2),
         te);
+    entry = lo;  // where the segment enters the grown box: the near-first order of the SAH walk
     return !(lo > hi);
 }
 
@@ -1167,6 +1168,14 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             T.found = leaf;
         }
     };
+    // SAH walk of plain-sphere worlds: two children per node step (below).  (Stack entries packing
+    // the pushed child's entry t, so that a pop skips children starting beyond te, lost 5 %: the
+    // skip loop's divergence costs more than the node steps it saves, profiles/r02/v9_two_child_ab.txt.)
+    constexpr bool C2 = TM == TM_SAH && LK == LK_SPHERES;
+    auto pop = [&]() {
+        if (T.sp == 0) T.phase = PH_SHADE;
+        else T.node = stack[(--T.sp) * RTW_BLOCK];
+    };
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
@@ -1237,8 +1246,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 float t;
                 if (leaf_t<STATS, LK == LK_ANY>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) take(t, leaf);
             }
-            if (T.sp == 0) T.phase = PH_SHADE;
-            else T.node = stack[(--T.sp) * RTW_BLOCK];
+            pop();
         }
         if (STATS) {
             const unsigned long long nm = __ballot(T.phase == ACT && T.node >= 0);
@@ -1247,12 +1255,41 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 db[DB_NODE_LANES] += (uint32_t)__popcll(nm);
             }
         }
+#ifndef RTW_SAH_ONE_CHILD
+        if (C2 && T.phase == ACT && T.node >= 0) {
+            // SAH walk, two children per step: the lane stands on a node already accepted (the root,
+            // or a child accepted by its parent's step) and tests both children's grown boxes at once
+            // (leaf children need no box: their own test follows); accepted children are visited
+            // near first (a leaf first), the other one pushed.  Any visit order finds the same
+            // closest root (§5.5 step 1), so only the work changes.
+            const float2 ch = reinterpret_cast<const float2*>(nodes_b)[2 * T.node + 1];
+            const int32_t left = __float_as_int(ch.x) >> 2, right = __float_as_int(ch.y);
+            const int32_t il = left >= 0 ? left : 0, ir = right >= 0 ? right : 0;
+            const float4 la = nodes_a[il], lb = nodes_b[il], ra = nodes_a[ir], rb = nodes_b[ir];
+            const float2 lk = nkm[il], rk = nkm[ir];
+            float el, er;
+            const bool pl = node_pass_cons(la, lb, lk, T.ray, rp, 0.001f, T.te, el) || left < 0;
+            const bool pr = node_pass_cons(ra, rb, rk, T.ray, rp, 0.001f, T.te, er) || right < 0;
+            if (left < 0) el = -F32_INF;
+            if (right < 0) er = -F32_INF;
+            if (pl && pr) {
+                const bool lf = el <= er;
+                stack[(T.sp++) * RTW_BLOCK] = (StackEntry)(lf ? right : left);
+                T.node = lf ? left : right;
+            } else if (pl || pr) {
+                T.node = pl ? left : right;
+            } else {
+                pop();
+            }
+        } else
+#endif
         if (T.phase == ACT && T.node >= 0) {
             if (STATS) st.c[ST_NODES]++;
             const float4 na = nodes_a[T.node];
             const float4 nb = nodes_b[T.node];
             const float2 km = nkm[T.node];
-            if (TM == TM_SAH ? node_pass_cons(na, nb, km, T.ray, rp, 0.001f, T.te)
+            float entry;
+            if (TM == TM_SAH ? node_pass_cons(na, nb, km, T.ray, rp, 0.001f, T.te, entry)
                              : node_pass<FAST_ONLY>(na, nb, km, T.ray, rp, 0.001f, T.te)) {
                 if (STATS) db[DB_PASS_LANES]++;
                 const int32_t lbits = __float_as_int(nb.z);
