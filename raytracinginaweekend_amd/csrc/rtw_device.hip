@@ -1223,7 +1223,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         // often.  That pays where leaf steps are a small share (final_scene1 ~0.1 leaf per node
         // step, suzanne ~0.4: +3 %, +5 %) and costs where leaves come at every turn (cornell_cube's
         // wall rects, ~0.8: -8 %), hence only for worlds without rect, box or wrapped leaves.
-        if ((STATS || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
+        // The two-children step of plain-sphere SAH walks (C2) halves the node steps between leaves:
+        // there a leaf body on every step is 3 % faster (profiles/r02/v9_leaf_cadence_ab.txt).
+        if ((STATS || C2 || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
             const int leaf = -1 - T.node;
             const float4 sph = fast[leaf];
             if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
