@@ -1156,13 +1156,11 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // DFS order) is seen and flagged
     auto take = [&](float t, int leaf) {
         if (TM == TM_SAH) {
-            if (T.found >= 0 && t == __int_as_float(__float_as_int(T.te) - 1)) {
-                T.fast |= RTW_TF_TIE;
-            } else {
-                T.te = __int_as_float(__float_as_int(t) + 1);  // t >= 0.001: the next float up
-                T.found = leaf;
-                T.fast &= ~RTW_TF_TIE;
-            }
+            // selects, not branches (+1.6 % on final_scene1: the branchy form cost exec-mask work)
+            const bool tie = T.found >= 0 && t == __int_as_float(__float_as_int(T.te) - 1);
+            T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
+            T.te = tie ? T.te : __int_as_float(__float_as_int(t) + 1);  // t >= 0.001: the next float up
+            T.found = tie ? T.found : leaf;
         } else {
             T.te = t;
             T.found = leaf;
