@@ -304,7 +304,10 @@ RTW_API int rtw_device_eval_scalar(int device, int fn, const float* a, const flo
 /* Device self-test of the traversal's node step (Aabb::hit_cond, aabb.rs:65-78, AND the proximity
  * cull): for each i, box[6i..] = min xyz, max xyz; ray[6i..] = origin xyz, direction xyz;
  * range[2i..] = t_start, t_end; km[2i..] = the node's cull constants; mk_world as computed at upload
- * (1: node coordinates admit the per-ray exact-division guard).  out[i] = 1 if the node passes. */
+ * (1: node coordinates admit the per-ray exact-division guard).  out[i] = 1 if the node passes.
+ * mk_world = 2 evaluates the SAH walk's node test instead (one-multiply quotients,
+ * constants widened x17/16 as uploaded) beside the cull alone with exact quotients: out[i] bit 0 =
+ * SAH test passes, bit 1 = exact cull passes, bit 2 = the ray admits the exact division. */
 RTW_API int rtw_device_eval_node_pass(int device, const float* box, const float* ray, const float* range,
                                       const float* km, int32_t mk_world, int64_t n, int32_t* out);
 

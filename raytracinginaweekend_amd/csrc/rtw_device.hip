@@ -765,6 +765,30 @@ __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, 
     return !(lo > hi);
 }
 
+// The cull alone with exact quotients and the plain constants (the SAH node test before the cheap
+// quotients; fast rays only): the reference the widened test must contain (eval_node_pass_kernel)
+__device__ __forceinline__ bool node_pass_cull_exact(float4 na, float4 nb, float2 km, const Ray& r, const RayPre& rp,
+                                                     float ts, float te) {
+    const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
+    const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
+    const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
+    const float delta = rtw_cull_delta(km.x, km.y, a0, b0, a1, b1, a2, b2);
+    const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
+    const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
+    const float qa2 = mk_div(a2, r.d.z, rp.inv.z), qb2 = mk_div(b2, r.d.z, rp.inv.z);
+    const float w0 = delta * __builtin_fabsf(rp.inv.x), w1 = delta * __builtin_fabsf(rp.inv.y),
+                w2 = delta * __builtin_fabsf(rp.inv.z);
+    const float lo = __builtin_fmaxf(
+        __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(qa0, qb0) - w0, __builtin_fminf(qa1, qb1) - w1),
+                        __builtin_fminf(qa2, qb2) - w2),
+        ts);
+    const float hi = __builtin_fminf(
+        __builtin_fminf(__builtin_fminf(__builtin_fmaxf(qa0, qb0) + w0, __builtin_fmaxf(qa1, qb1) + w1),
+                        __builtin_fmaxf(qa2, qb2) + w2),
+        te);
+    return !(lo > hi);
+}
+
 // Aabb::hit_cond (aabb.rs:65-78) alone, exact quotients (fast rays only): node_pass's first half
 __device__ __forceinline__ bool box_hit_cond_fast(float4 na, float4 nb, const Ray& r, const RayPre& rp, float ts,
                                                   float te) {
@@ -1838,10 +1862,22 @@ __global__ void eval_node_pass_kernel(const float* box, const float* ray, const 
     R.d = v3(r[3], r[4], r[5]);
     R.time = 0.0f;
     const RayPre rp = ray_pre(R, mk_world != 0);
-    out[i] = node_pass(make_float4(b[0], b[1], b[2], b[3]), make_float4(b[4], b[5], 0.0f, 0.0f),
-                       make_float2(km[2 * i], km[2 * i + 1]), R, rp, range[2 * i], range[2 * i + 1])
-                 ? 1
-                 : 0;
+    const float4 na = make_float4(b[0], b[1], b[2], b[3]), nb = make_float4(b[4], b[5], 0.0f, 0.0f);
+    if (mk_world == 2) {
+        // the SAH walk's node test (cheap quotients, constants widened as build_sah_tables uploads
+        // them) beside the cull alone with exact quotients and the plain constants: bit 0 = SAH test
+        // passes, bit 1 = exact cull passes, bit 2 = the ray is Markstein-exact (the SAH walk's rays)
+        float k = km[2 * i], m = km[2 * i + 1];
+        if (k > 0.0f) k = nextafterf(k * RTW_SAH_WIDEN, F32_INF);
+        if (m > 0.0f) m = nextafterf(m * RTW_SAH_WIDEN, F32_INF);
+        float e;
+        const bool sah = node_pass_cons(na, nb, make_float2(k, m), R, rp, range[2 * i], range[2 * i + 1], e);
+        const bool exact = node_pass_cull_exact(na, nb, make_float2(km[2 * i], km[2 * i + 1]), R, rp, range[2 * i],
+                                                range[2 * i + 1]);
+        out[i] = (sah ? 1 : 0) | (exact ? 2 : 0) | (rp.fast ? 4 : 0);
+        return;
+    }
+    out[i] = node_pass(na, nb, make_float2(km[2 * i], km[2 * i + 1]), R, rp, range[2 * i], range[2 * i + 1]) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
