@@ -1320,7 +1320,10 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 const int32_t left = lbits >> 2;
                 const int axis = lbits & 3;
                 const int32_t right = __float_as_int(nb.w);
-                const bool fwd = __builtin_amdgcn_ubfe((uint32_t)T.fast, (uint32_t)axis, 1u) != 0u;  // ray.d[axis] > 0
+                bool fwd = __builtin_amdgcn_ubfe((uint32_t)T.fast, (uint32_t)axis, 1u) != 0u;  // ray.d[axis] > 0
+                // SAH walk: a leaf child first (its hit shrinks te before the sibling subtree; suzanne
+                // +2.2 %, profiles/r02/v9_two_child_ab.txt)
+                if (TM == TM_SAH && (left < 0) != (right < 0)) fwd = left < 0;
                 // hit_index_list order: near subtree, then far
                 stack[(T.sp++) * RTW_BLOCK] = (StackEntry)(fwd ? right : left);
                 T.node = fwd ? left : right;
