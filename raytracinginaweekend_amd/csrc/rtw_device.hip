@@ -1239,7 +1239,12 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 #define RTW_TRAV_UNROLL 6
 #endif
 #pragma unroll
-        for (int u = 0; u < (STATS ? 1 : RTW_TRAV_UNROLL); ++u) {
+// the two-children walk has the costlier step: 3 steps per check there (+1.0 % over 6 on
+// final_scene1, 4: +0.5 %, profiles/r02/v9_take_unroll_ab.txt)
+#ifndef RTW_C2_UNROLL
+#define RTW_C2_UNROLL 3
+#endif
+        for (int u = 0; u < (STATS ? 1 : C2 ? RTW_C2_UNROLL : RTW_TRAV_UNROLL); ++u) {
         // leaf bodies on every step, or (LK_SPHERES, LK_TRIS) on even steps only: a lane reaching a
         // leaf then waits up to one step, and the wave runs a leaf body for twice the lanes half as
         // often.  That pays where leaf steps are a small share (final_scene1 ~0.1 leaf per node
