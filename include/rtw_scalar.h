@@ -12,9 +12,9 @@
  *      of how pixels are spread over lanes, threads or GPUs.
  *   3. f32 elementary functions used on the device path (acos/atan2 for sphere uv
  *      `vec3.rs:241-249`, ln for volumes `hittable.rs:328`, sin for checker/marble
- *      `texture.rs:32,50`).  The reference calls the platform libm (glibc); these are evaluated in
- *      f64 and rounded once, i.e. correctly rounded except in double-rounding hard cases
- *      (probability ~2^-29 per call).  Tested against numpy f64 in tests/test_scalar.py.
+ *      `texture.rs:32,50`).  The reference calls the platform libm; these restate glibc 2.35's
+ *      acosf / atan2f / sinf / logf (the FMA builds x86-64 selects) bit for bit, pinned
+ *      exhaustively against the live libm (tests/test_libm.py).
  *   4. Rust-semantics helpers: f32::min/max (NaN-ignoring), saturating `as` casts, minmax.
  *
  * Everything else (geometry, BVH traversal, materials, the bounce loop) is implemented
@@ -283,194 +283,292 @@ RTW_HD uint32_t rtw_gen_range_u32(uint32_t n, rtw_xoro* r) {
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* f32 elementary functions, evaluated in f64 and rounded once                                */
+/* f32 elementary functions: glibc 2.35's libm, restated bit for bit                          */
 /* ------------------------------------------------------------------------------------------ */
-#define RTW_PI_D 3.141592653589793115997963468544185161590576171875
-#define RTW_PIO2_D 1.5707963267948965579989817342720925807952880859375
-#define RTW_PIO6_D 0.52359877559829881565889309058547951281070709228515625
-#define RTW_SQRT3_D 1.732050807568877193176604123436845839023590087890625
-#define RTW_LN2_D 0.69314718055994528622676398299518041312694549560546875
+/* The reference calls f32::acos / atan2 (vec3.rs:242-243, every sphere uv), f32::sin
+ * (texture.rs:32 checker, :50 marble) and f32::ln (hittable.rs:328, volume distance).  On Linux
+ * Rust lowers them to the platform libm's acosf / atan2f / sinf / logf.  The platform here is
+ * glibc 2.35 (Ubuntu 22.04, this image and the GPU box), x86-64 with FMA, where the dynamic
+ * linker's ifunc picks the FMA builds of sinf and logf.  None of the four is correctly rounded
+ * (acosf differs from RN(acos) on ~8 % of [-1, 1], atan2f on ~16 %), so the restatement follows
+ * glibc's own algorithms and operation order:
+ *   acosf   sysdeps/ieee754/flt-32/e_acosf.c   (fdlibm, f32 arithmetic)
+ *   atan2f  sysdeps/ieee754/flt-32/e_atan2f.c  (fdlibm) + s_atanf.c
+ *   sinf    sysdeps/ieee754/flt-32/s_sinf.c + sincosf.h + sincosf_data.c  (f64 kernels, FMA build)
+ *   logf    sysdeps/ieee754/flt-32/e_logf.c + e_logf_data.c             (f64 kernel, FMA build)
+ * The FMA builds contract specific multiply-adds; each rtw_fma below marks one of them.  Pinned
+ * exhaustively against the live libm (tests/native/libm_check.c: every f32 input of acosf, sinf
+ * and logf, 2^28 atan2f pairs; 0 mismatches) and by tests/golden/libm_f32.npz. */
+RTW_HD double rtw_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
-/* atan on doubles; |error| ~ 1e-16 relative.  Reduction: |x|>1 -> pi/2 - atan(1/x);
- * x > tan(pi/12) -> pi/6 + atan((x*sqrt3 - 1)/(x + sqrt3)); then the Taylor series. */
-RTW_HD double rtw_atan_d(double x) {
-    const int neg = x < 0.0;
-    if (neg) x = -x;
-    int inv = 0;
-    if (x > 1.0) {
-        x = 1.0 / x;
-        inv = 1;
-    }
-    double off = 0.0;
-    if (x > 0.26794919243112270) {
-        x = (x * RTW_SQRT3_D - 1.0) / (x + RTW_SQRT3_D);
-        off = RTW_PIO6_D;
-    }
-    const double x2 = x * x;
-    /* sum_{k=0..16} (-1)^k x^(2k+1) / (2k+1); |x| <= 0.268 -> truncation < 1e-20 */
-    double p = -1.0 / 33.0;
-    p = p * x2 + 1.0 / 31.0;
-    p = p * x2 - 1.0 / 29.0;
-    p = p * x2 + 1.0 / 27.0;
-    p = p * x2 - 1.0 / 25.0;
-    p = p * x2 + 1.0 / 23.0;
-    p = p * x2 - 1.0 / 21.0;
-    p = p * x2 + 1.0 / 19.0;
-    p = p * x2 - 1.0 / 17.0;
-    p = p * x2 + 1.0 / 15.0;
-    p = p * x2 - 1.0 / 13.0;
-    p = p * x2 + 1.0 / 11.0;
-    p = p * x2 - 1.0 / 9.0;
-    p = p * x2 + 1.0 / 7.0;
-    p = p * x2 - 1.0 / 5.0;
-    p = p * x2 + 1.0 / 3.0;
-    double r = off + (x - x * x2 * p);
-    if (inv) r = RTW_PIO2_D - r;
-    return neg ? -r : r;
-}
-
-/* atan2f with C99 special cases (what Rust's f32::atan2 gets from libm). */
-RTW_HD float rtw_atan2f(float y, float x) {
-    if (x != x || y != y) return x + y;
-    const int ysign = (rtw_f2u(y) >> 31) != 0;
-    const int xsign = (rtw_f2u(x) >> 31) != 0;
-    const float INF = rtw_u2f(0x7F800000u);
-    if (y == 0.0f) {
-        if (!xsign) return y;                      /* atan2(+-0, +x or +0) = +-0 */
-        return ysign ? (float)-RTW_PI_D : (float)RTW_PI_D;
-    }
-    if (x == 0.0f) return ysign ? (float)-RTW_PIO2_D : (float)RTW_PIO2_D;
-    if (x == INF || x == -INF) {
-        if (y == INF || y == -INF) {
-            const double a = xsign ? 3.0 * RTW_PI_D / 4.0 : RTW_PI_D / 4.0;
-            return (float)(ysign ? -a : a);
-        }
-        if (!xsign) return ysign ? -0.0f : 0.0f;
-        return ysign ? (float)-RTW_PI_D : (float)RTW_PI_D;
-    }
-    if (y == INF || y == -INF) return ysign ? (float)-RTW_PIO2_D : (float)RTW_PIO2_D;
-    const double yd = y < 0.0f ? -(double)y : (double)y;
-    const double xd = x < 0.0f ? -(double)x : (double)x;
-    double a = rtw_atan_d(yd / xd);
-    if (xsign) a = RTW_PI_D - a;
-    return (float)(ysign ? -a : a);
-}
-
-/* acosf: 2*atan(sqrt((1-x)/(1+x))); |x| > 1 or NaN -> NaN. */
+/* e_acosf.c __ieee754_acosf */
 RTW_HD float rtw_acosf(float x) {
-    if (x != x) return x;
-    if (x > 1.0f || x < -1.0f) return rtw_u2f(0x7FC00000u);
-    const double xd = (double)x;
-    const double q = (1.0 - xd) / (1.0 + xd); /* x = -1 -> +inf -> atan = pi/2 */
-    return (float)(2.0 * rtw_atan_d(__builtin_sqrt(q)));
+    const float one = 1.0f, half = 0.5f;
+    const float pi = rtw_u2f(0x40490fdau), pio2_hi = rtw_u2f(0x3fc90fdau), pio2_lo = rtw_u2f(0x33a22168u);
+    const float pS0 = rtw_u2f(0x3e2aaaabu), pS1 = rtw_u2f(0xbea6b090u), pS2 = rtw_u2f(0x3e4e0aa8u),
+                pS3 = rtw_u2f(0xbd241146u), pS4 = rtw_u2f(0x3a4f7f04u), pS5 = rtw_u2f(0x3811ef08u);
+    const float qS1 = rtw_u2f(0xc019d139u), qS2 = rtw_u2f(0x4001572du), qS3 = rtw_u2f(0xbf303361u),
+                qS4 = rtw_u2f(0x3d9dc62eu);
+    const int32_t hx = (int32_t)rtw_f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    float z, p, q, r, w, s;
+    if (ix == 0x3f800000) {                               /* |x| == 1 */
+        if (hx > 0) return 0.0f;
+        return pi + rtw_u2f(0x34222168u);                 /* pi + 2 pio2_lo */
+    }
+    if (ix > 0x3f800000) return (x - x) / (x - x);        /* |x| > 1 or NaN */
+    if (ix < 0x3f000000) {                                /* |x| < 0.5 */
+        if (ix <= 0x32800000) return pio2_hi + pio2_lo;   /* |x| <= 2^-26 */
+        z = x * x;
+        p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        r = p / q;
+        return pio2_hi - (x - (pio2_lo - x * r));
+    } else if (hx < 0) {                                  /* x < -0.5 */
+        z = (one + x) * half;
+        p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        s = __builtin_sqrtf(z);
+        r = p / q;
+        w = r * s - pio2_lo;
+        return pi - 2.0f * (s + w);
+    } else {                                              /* x > 0.5 */
+        z = (one - x) * half;
+        s = __builtin_sqrtf(z);
+        const float df = rtw_u2f(rtw_f2u(s) & 0xfffff000u);
+        const float c = (z - df * df) / (s + df);
+        p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        r = p / q;
+        w = r * s + c;
+        return 2.0f * (df + w);
+    }
 }
 
-/* lnf (Rust f32::ln): m in [sqrt(2)/2, sqrt(2)), ln m = 2 atanh(f/(2+f)). */
+/* s_atanf.c __atanf */
+RTW_HD float rtw_atanf(float x) {
+    const float one = 1.0f;
+    const float atanhi[4] = {rtw_u2f(0x3eed6338u), rtw_u2f(0x3f490fdau), rtw_u2f(0x3f7b985eu), rtw_u2f(0x3fc90fdau)};
+    const float atanlo[4] = {rtw_u2f(0x31ac3769u), rtw_u2f(0x33222168u), rtw_u2f(0x33140fb4u), rtw_u2f(0x33a22168u)};
+    const float aT0 = rtw_u2f(0x3eaaaaabu), aT1 = rtw_u2f(0xbe4ccccdu), aT2 = rtw_u2f(0x3e124925u),
+                aT3 = rtw_u2f(0xbde38e38u), aT4 = rtw_u2f(0x3dba2e6eu), aT5 = rtw_u2f(0xbd9d8795u),
+                aT6 = rtw_u2f(0x3d886b35u), aT7 = rtw_u2f(0xbd6ef16bu), aT8 = rtw_u2f(0x3d4bda59u),
+                aT9 = rtw_u2f(0xbd15a221u), aT10 = rtw_u2f(0x3c8569d7u);
+    const int32_t hx = (int32_t)rtw_f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {                               /* |x| >= 2^25 */
+        if (ix > 0x7f800000) return x + x;                /* NaN */
+        if (hx > 0) return atanhi[3] + atanlo[3];
+        return -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) {                                /* |x| < 0.4375 */
+        if (ix < 0x31000000) return x;                    /* |x| < 2^-29 */
+        id = -1;
+    } else {
+        x = __builtin_fabsf(x);
+        if (ix < 0x3f980000) {                            /* |x| < 1.1875 */
+            if (ix < 0x3f300000) {                        /* 7/16 <= |x| < 11/16 */
+                id = 0;
+                x = (2.0f * x - one) / (2.0f + x);
+            } else {                                      /* 11/16 <= |x| < 19/16 */
+                id = 1;
+                x = (x - one) / (x + one);
+            }
+        } else if (ix < 0x401c0000) {                     /* |x| < 2.4375 */
+            id = 2;
+            x = (x - 1.5f) / (one + 1.5f * x);
+        } else {                                          /* 2.4375 <= |x| < 2^25 */
+            id = 3;
+            x = -1.0f / x;
+        }
+    }
+    const float z = x * x;
+    const float w = z * z;
+    const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return (hx < 0) ? -r : r;
+}
+
+/* e_atan2f.c __ieee754_atan2f (the w_atan2f wrapper only sets errno) */
+RTW_HD float rtw_atan2f(float y, float x) {
+    const float tiny = rtw_u2f(0x0da24260u);              /* 1.0e-30 */
+    const float pi_o_4 = rtw_u2f(0x3f490fdbu), pi_o_2 = rtw_u2f(0x3fc90fdbu), pi = rtw_u2f(0x40490fdbu),
+                pi_lo = rtw_u2f(0xb3bbbd2eu);
+    const int32_t hx = (int32_t)rtw_f2u(x), hy = (int32_t)rtw_f2u(y);
+    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y; /* NaN */
+    if (hx == 0x3f800000) return rtw_atanf(y);            /* x = 1 */
+    const int m = (int)(((uint32_t)hy >> 31) & 1u) | (int)(((uint32_t)hx >> 30) & 2u);
+    if (iy == 0) {
+        switch (m) {
+            case 0:
+            case 1: return y;
+            case 2: return pi + tiny;
+            default: return -pi - tiny;
+        }
+    }
+    if (ix == 0) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            switch (m) {
+                case 0: return pi_o_4 + tiny;
+                case 1: return -pi_o_4 - tiny;
+                case 2: return 3.0f * pi_o_4 + tiny;
+                default: return -3.0f * pi_o_4 - tiny;
+            }
+        }
+        switch (m) {
+            case 0: return 0.0f;
+            case 1: return -0.0f;
+            case 2: return pi + tiny;
+            default: return -pi - tiny;
+        }
+    }
+    if (iy == 0x7f800000) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;                /* |y/x| > 2^60 */
+    else if (hx < 0 && k < -60) z = 0.0f;                 /* |y|/x < -2^60 */
+    else z = rtw_atanf(__builtin_fabsf(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return rtw_u2f(rtw_f2u(z) ^ 0x80000000u);
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
+/* e_logf.c __logf with e_logf_data.c (LOGF_TABLE_BITS 4, poly order 4); FMA build. */
 RTW_HD float rtw_logf(float x) {
-    if (x != x) return x;
-    if (x < 0.0f) return rtw_u2f(0x7FC00000u);
-    if (x == 0.0f) return rtw_u2f(0xFF800000u);
-    if (x == rtw_u2f(0x7F800000u)) return x;
-    const double d = (double)x; /* every f32 (subnormals included) is a normal f64 */
-    const uint64_t u = rtw_d2u(d);
-    int e = (int)((u >> 52) & 0x7FF) - 1023;
-    double m = rtw_u2d((u & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
-    if (m > 1.4142135623730951) {
-        m = m * 0.5;
-        e += 1;
+    /* {invc, logc}: 1/c and log(c) for the 16 subintervals of [0x3f330000, 2 * 0x3f330000) */
+    const uint64_t T[16][2] = {
+        {0x3ff661ec79f8f3beull, 0xbfd57bf7808caadeull}, {0x3ff571ed4aaf883dull, 0xbfd2bef0a7c06ddbull},
+        {0x3ff49539f0f010b0ull, 0xbfd01eae7f513a67ull}, {0x3ff3c995b0b80385ull, 0xbfcb31d8a68224e9ull},
+        {0x3ff30d190c8864a5ull, 0xbfc6574f0ac07758ull}, {0x3ff25e227b0b8ea0ull, 0xbfc1aa2bc79c8100ull},
+        {0x3ff1bb4a4a1a343full, 0xbfba4e76ce8c0e5eull}, {0x3ff12358f08ae5baull, 0xbfb1973c5a611cccull},
+        {0x3ff0953f419900a7ull, 0xbfa252f438e10c1eull}, {0x3ff0000000000000ull, 0x0000000000000000ull},
+        {0x3fee608cfd9a47acull, 0x3faaa5aa5df25984ull}, {0x3feca4b31f026aa0ull, 0x3fbc5e53aa362eb4ull},
+        {0x3feb2036576afce6ull, 0x3fc526e57720db08ull}, {0x3fe9c2d163a1aa2dull, 0x3fcbc2860d224770ull},
+        {0x3fe886e6037841edull, 0x3fd1058bc8a07ee1ull}, {0x3fe767dcf5534862ull, 0x3fd4043057b6ee09ull}};
+    const double Ln2 = rtw_u2d(0x3fe62e42fefa39efull);
+    const double A0 = rtw_u2d(0xbfd00ea348b88334ull), A1 = rtw_u2d(0x3fd5575b0be00b6aull),
+                 A2 = rtw_u2d(0xbfdffffef20a4123ull);
+    uint32_t ix = rtw_f2u(x);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) { /* subnormal, zero, negative, inf, NaN */
+        if (ix * 2u == 0u) return rtw_u2f(0xff800000u);    /* -inf (divide by zero) */
+        if (ix == 0x7f800000u) return x;                  /* log(inf) = inf */
+        if ((ix & 0x80000000u) || ix * 2u >= 0xff000000u) return (x - x) / (x - x);
+        ix = rtw_f2u(x * 0x1p23f);                        /* subnormal: normalise */
+        ix -= 23u << 23;
     }
-    const double f = m - 1.0;
-    const double s = f / (2.0 + f);
-    const double s2 = s * s;
-    /* 2*(s + s^3/3 + ... + s^25/25); |s| <= 0.1716 -> truncation < 1e-20 */
-    double p = 1.0 / 25.0;
-    p = p * s2 + 1.0 / 23.0;
-    p = p * s2 + 1.0 / 21.0;
-    p = p * s2 + 1.0 / 19.0;
-    p = p * s2 + 1.0 / 17.0;
-    p = p * s2 + 1.0 / 15.0;
-    p = p * s2 + 1.0 / 13.0;
-    p = p * s2 + 1.0 / 11.0;
-    p = p * s2 + 1.0 / 9.0;
-    p = p * s2 + 1.0 / 7.0;
-    p = p * s2 + 1.0 / 5.0;
-    p = p * s2 + 1.0 / 3.0;
-    const double lm = 2.0 * (s + s * s2 * p);
-    return (float)((double)e * RTW_LN2_D + lm);
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) % 16u);
+    const int32_t k = (int32_t)tmp >> 23;                 /* arithmetic shift */
+    const uint32_t iz = ix - (tmp & 0xff800000u);
+    const double invc = rtw_u2d(T[i][0]), logc = rtw_u2d(T[i][1]);
+    const double z = (double)rtw_u2f(iz);
+    const double r = rtw_fma(z, invc, -1.0);              /* z * invc - 1 */
+    const double y0 = rtw_fma((double)k, Ln2, logc);      /* logc + k * Ln2 */
+    const double r2 = r * r;
+    double y = rtw_fma(A1, r, A2);                        /* A[1] * r + A[2] */
+    y = rtw_fma(A0, r2, y);                               /* A[0] * r2 + y */
+    y = rtw_fma(y, r2, y0 + r);                           /* y * r2 + (y0 + r) */
+    return (float)y;
 }
 
-/* sinf: Cody-Waite reduction by pi/2 in f64 (exact for |x| < 2^20 * pi/2), Taylor kernels. */
-RTW_HD double rtw_sin_kernel_d(double r) {
-    /* sin r = sum_{k>=0} (-1)^k r^(2k+1)/(2k+1)!, k = 0..9; |r| <= pi/4 -> truncation < 1e-19 */
-    const double r2 = r * r;
-    const double c9 = -1.0 / 121645100408832000.0;
-    const double c8 = 1.0 / 355687428096000.0;
-    const double c7 = -1.0 / 1307674368000.0;
-    const double c6 = 1.0 / 6227020800.0;
-    const double c5 = -1.0 / 39916800.0;
-    const double c4 = 1.0 / 362880.0;
-    const double c3 = -1.0 / 5040.0;
-    const double c2 = 1.0 / 120.0;
-    const double c1 = -1.0 / 6.0;
-    double t = c9;
-    t = t * r2 + c8;
-    t = t * r2 + c7;
-    t = t * r2 + c6;
-    t = t * r2 + c5;
-    t = t * r2 + c4;
-    t = t * r2 + c3;
-    t = t * r2 + c2;
-    t = t * r2 + c1;
-    return r + r * r2 * t;
+/* sincosf_data.c __sincosf_table[0] (quadrants 0, 1) and [1] (2, 3): the sine coefficients are
+ * shared, the cosine ones negated in [1].  {c0, c1, s1, c2, s2, c3, s3, c4}. */
+RTW_HD double rtw_sincosf_coef(int table, int j) {
+    const uint64_t C[2][8] = {
+        {0x3ff0000000000000ull, 0xbfdffffffd0c621cull, 0xbfc555545995a603ull, 0x3fa55553e1068f19ull,
+         0x3f81107605230bc4ull, 0xbf56c087e89a359dull, 0xbf2994eb3774cf24ull, 0x3ef99343027bf8c3ull},
+        {0xbff0000000000000ull, 0x3fdffffffd0c621cull, 0xbfc555545995a603ull, 0xbfa55553e1068f19ull,
+         0x3f81107605230bc4ull, 0x3f56c087e89a359dull, 0xbf2994eb3774cf24ull, 0xbef99343027bf8c3ull}};
+    return rtw_u2d(C[table][j]);
 }
-RTW_HD double rtw_cos_kernel_d(double r) {
-    const double r2 = r * r;
-    /* cos r = sum_{k>=0} (-1)^k r^(2k)/(2k)!, k = 0..10 */
-    const double c10 = 1.0 / 2432902008176640000.0;
-    const double c9 = -1.0 / 6402373705728000.0;
-    const double c8 = 1.0 / 20922789888000.0;
-    const double c7 = -1.0 / 87178291200.0;
-    const double c6 = 1.0 / 479001600.0;
-    const double c5 = -1.0 / 3628800.0;
-    const double c4 = 1.0 / 40320.0;
-    const double c3 = -1.0 / 720.0;
-    const double c2 = 1.0 / 24.0;
-    const double c1 = -1.0 / 2.0;
-    double t = c10;
-    t = t * r2 + c9;
-    t = t * r2 + c8;
-    t = t * r2 + c7;
-    t = t * r2 + c6;
-    t = t * r2 + c5;
-    t = t * r2 + c4;
-    t = t * r2 + c3;
-    t = t * r2 + c2;
-    t = t * r2 + c1;
-    return 1.0 + r2 * t;
+/* sincosf.h sinf_poly: n even -> sine polynomial of x (x2 = x*x of the unsigned remainder),
+ * n odd -> cosine polynomial; FMA build. */
+RTW_HD float rtw_sinf_poly(double x, double x2, int table, int n) {
+    if ((n & 1) == 0) {
+        const double x3 = x * x2;
+        const double s1 = rtw_fma(x2, rtw_sincosf_coef(table, 6), rtw_sincosf_coef(table, 4)); /* s2 + x2 s3 */
+        const double x7 = x3 * x2;
+        const double s = rtw_fma(x3, rtw_sincosf_coef(table, 2), x);                            /* x + x3 s1 */
+        return (float)rtw_fma(x7, s1, s);
+    }
+    const double x4 = x2 * x2;
+    const double c2 = rtw_fma(x2, rtw_sincosf_coef(table, 7), rtw_sincosf_coef(table, 5));     /* c3 + x2 c4 */
+    const double c1 = rtw_fma(x2, rtw_sincosf_coef(table, 1), rtw_sincosf_coef(table, 0));     /* c0 + x2 c1 */
+    const double x6 = x4 * x2;
+    const double c = rtw_fma(x4, rtw_sincosf_coef(table, 3), c1);                               /* c1 + x4 c2 */
+    return (float)rtw_fma(x6, c2, c);
 }
-RTW_HD float rtw_sinf(float x) {
-    if (x != x) return x;
-    if (x == rtw_u2f(0x7F800000u) || x == rtw_u2f(0xFF800000u)) return rtw_u2f(0x7FC00000u);
-    if (x == 0.0f) return x; /* keeps the sign of zero */
-    const double d = (double)x;
-    /* k = round(d * 2/pi) */
+/* sincosf.h reduce_large: x * 4/pi in 2.62 fixed point from __inv_pio4 (the bits of 4/pi),
+ * for 120 <= |x| < inf; returns the remainder in radians, n = the quadrant. */
+RTW_HD double rtw_sinf_reduce_large(uint32_t xi, int* np) {
+    const uint32_t inv_pio4[24] = {
+        0xa2u, 0xa2f9u, 0xa2f983u, 0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u, 0x6e4e4415u, 0x4e441529u,
+        0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u, 0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u,
+        0x34ddc0dbu, 0xddc0db62u, 0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
+    const uint32_t* arr = &inv_pio4[(xi >> 26) & 15u];
+    const int shift = (int)((xi >> 23) & 7u);
+    xi = (xi & 0xffffffu) | 0x800000u;
+    xi <<= shift;
+    uint64_t res0 = (uint64_t)(uint32_t)(xi * arr[0]);
+    const uint64_t res1 = (uint64_t)xi * arr[4];
+    const uint64_t res2 = (uint64_t)xi * arr[8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    const uint64_t n = (res0 + (1ull << 61)) >> 62;
+    res0 -= n << 62;
+    *np = (int)n;
+    return (double)(int64_t)res0 * rtw_u2d(0x3c1921fb54442d18ull); /* pi / 2^63 */
+}
+/* s_sinf.c sinf; FMA build. */
+RTW_HD float rtw_sinf(float y) {
+    const double sign[4] = {1.0, -1.0, -1.0, 1.0};
+    double x = (double)y;
+    const uint32_t top = (rtw_f2u(y) >> 20) & 0x7ffu;
+    if (top < 0x3f4u) {                                   /* |y| < pi/4 */
+        if (top < 0x398u) return y;                       /* |y| < 2^-12 */
+        return rtw_sinf_poly(x, x * x, 0, 0);
+    }
+    if (top < 0x42fu) {                                   /* |y| < 120: reduce_fast */
+        const double r = x * rtw_u2d(0x41645f306dc9c883ull);     /* x * 2/pi * 2^24 */
+        const int n = ((int32_t)r + 0x800000) >> 24;
+        x = rtw_fma(-(double)n, rtw_u2d(0x3ff921fb54442d18ull), x); /* x - n pi/2 */
+        return rtw_sinf_poly(x * sign[n & 3], x * x, (n & 2) ? 1 : 0, n);
+    }
+    if (top < 0x7f8u) {                                   /* finite */
+        const uint32_t xi = rtw_f2u(y);
+        const int s = (int)(xi >> 31);
+        int n;
+        x = rtw_sinf_reduce_large(xi, &n);
+        return rtw_sinf_poly(x * sign[(n + s) & 3], x * x, ((n + s) & 2) ? 1 : 0, n);
+    }
+    return (y - y) / (y - y);                             /* inf, NaN */
+}
+
+/* CheckerTexture reads only the sign of RN(RN(sin x sin y) sin z) (texture.rs:32-33).  The sign
+ * of one sine follows from a Cody-Waite reduction x = k pi/2 + r (three-part pi/2, exact for
+ * |x| < 2^19) whenever |r| > 2^-30: sin x then has the sign of sin r, cos r > 0, -sin r or -cos r
+ * for k = 0, 1, 2, 3 mod 4, and |sin x| > 2^-31, so glibc's sinf (error < 1 ulp) has that sign and
+ * none of the two f32 products is zero or subnormal.  Returns 1 and sets *neg when decided, 0 when
+ * the sine must be evaluated (0, |x| >= 2^19, NaN, x next to a multiple of pi/2).  Pinned against
+ * the live libm's sinf sign for every f32 (tests/native/libm_check.c mode sinsign). */
+RTW_HD int rtw_sin_sign_fast(float x, int* neg) {
+    const double d = __builtin_fabs((double)x) < 0x1p19 ? (double)x : 0.0; /* NaN, huge -> 0 */
     const double kd = __builtin_rint(d * 0.63661977236758138243);
-    /* pi/2 split into three parts; PIO2_1 has 33 significant bits (k*PIO2_1 exact for |k|<2^20) */
-    const double PIO2_1 = 1.57079632673412561417e+00; /* 0x3FF921FB54400000 */
-    const double PIO2_2 = 6.07710050630396597660e-11; /* 0x3DD0B4611A600000 */
-    const double PIO2_3 = 2.02226624871116645580e-21; /* 0x3BA3198A2E000000 */
-    const double r = ((d - kd * PIO2_1) - kd * PIO2_2) - kd * PIO2_3;
-    const int64_t k = (int64_t)kd;
-    double v;
-    switch ((int)(k & 3)) {
-        case 0: v = rtw_sin_kernel_d(r); break;
-        case 1: v = rtw_cos_kernel_d(r); break;
-        case 2: v = -rtw_sin_kernel_d(r); break;
-        default: v = -rtw_cos_kernel_d(r); break;
-    }
-    return (float)v;
+    const double r = ((d - kd * 1.57079632673412561417e+00) - kd * 6.07710050630396597660e-11) -
+                     kd * 2.02226624871116645580e-21;
+    const int q = (int)kd & 3;
+    *neg = (q == 0) ? r < 0.0 : (q == 2) ? r > 0.0 : q == 3;
+    return __builtin_fabs(r) > 0x1p-30;                   /* d = 0 (also 0, NaN, huge x): undecided */
 }
-
 
 /* ------------------------------------------------------------------------------------------ */
 /* Proximity cull (ours, not in the reference): an extra per-node test ANDed with the          */

@@ -233,23 +233,16 @@ __device__ __noinline__ float d_logf(float x) { return rtw_logf(x); }
 __device__ __noinline__ float d_sinf(float x) { return rtw_sinf(x); }
 
 // CheckerTexture's test (texture.rs:33-40): is RN(RN(sinf(x) * sinf(y)) * sinf(z)) < 0?  Only the
-// sign of the product is read, so the sines' polynomials are not needed when rtw_sinf's own
-// reduction (x = k pi/2 + r, exact for |x| < 2^19) leaves |r| > 2^-30: each sine then has the sign
-// its quadrant and r give (sin r for k = 0 mod 4, cos r > 0 for 1, -sin r for 2, -cos r for 3;
-// |r| <= pi/4) and magnitude > 2^-31, so neither f32 product is zero, subnormal or of another
-// sign, and the result is negative iff an odd number of the sines are.  Other arguments (0,
-// huge, NaN, near a multiple of pi) evaluate the sines.
+// sign of the product is read: when rtw_sin_sign_fast decides all three sines' signs (rtw_scalar.h,
+// pinned against glibc's sinf for every f32), the product is negative iff an odd number of them
+// are.  Other arguments (0, huge, NaN, near a multiple of pi/2) evaluate the sines.
 __device__ __noinline__ bool d_checker_odd(float x, float y, float z) {
     const float c[3] = {x, y, z};
     bool fast = true, odd = false;
     for (int i = 0; i < 3; ++i) {
-        const double d = (double)c[i];
-        const double kd = __builtin_rint(d * 0.63661977236758138243);
-        const double r = ((d - kd * 1.57079632673412561417e+00) - kd * 6.07710050630396597660e-11) -
-                         kd * 2.02226624871116645580e-21;
-        fast = fast && __builtin_fabs(d) < 0x1p19 && __builtin_fabs(r) > 0x1p-30;
-        const int q = (int)kd & 3;  // |kd| < 2^19 on the fast path
-        odd ^= (q == 0) ? r < 0.0 : (q == 2) ? r > 0.0 : q == 3;
+        int neg;
+        fast = rtw_sin_sign_fast(c[i], &neg) && fast;
+        odd ^= neg != 0;
     }
     if (fast) return odd;
     return d_sinf(x) * d_sinf(y) * d_sinf(z) < 0.0f;
