@@ -561,7 +561,7 @@ pub fn render_gpu_seeded(image_size: Size2i, thread_count: usize, samples_per_pi
     let p = RtwRenderParams {
         width: image_size.width,
         height: image_size.height,
-        samples_per_pixel: samples_per_pixel as u32,
+        samples_per_pixel: u32::try_from(samples_per_pixel).expect("samples_per_pixel exceeds u32::MAX"),
         max_depth,
         render_mode: match render_mode {
             RenderMode::Default => RTW_MODE_DEFAULT,

@@ -869,6 +869,7 @@ static int validate(const rtw_world* w, const rtw_render_params* p) {
     if (w->leaf_count < 1) return RTW_ERR_INVALID_ARGUMENT;
     const int pc = p->part_count > 0 ? p->part_count : 1;
     if (p->part_index < 0 || p->part_index >= pc) return RTW_ERR_INVALID_ARGUMENT;
+    if (p->thread_count < 0 || p->reserved0 != 0) return RTW_ERR_INVALID_ARGUMENT; /* as the device */
     return RTW_OK;
 }
 

@@ -314,8 +314,15 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if not os.environ.get("RTW_LIBRARY") and L.rtw_version() != ABI_VERSION:
-            raise ImportError(f"{LIB_PATH} has ABI version {L.rtw_version()}, this package needs {ABI_VERSION}: rebuild it")
+        if L.rtw_version() != ABI_VERSION:
+            msg = f"{LIB_PATH} has ABI version {L.rtw_version()}, this package needs {ABI_VERSION}"
+            if not os.environ.get("RTW_LIBRARY"):
+                raise ImportError(msg + ": rebuild it")
+            # experiment builds (RTW_LIBRARY) may predate an ABI change: say so instead of rendering
+            # with a misread rtw_render_params
+            import warnings
+
+            warnings.warn(msg + " (RTW_LIBRARY override): thread_count and later fields are not honoured")
         _lib = L
     return _lib
 

@@ -670,7 +670,10 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
         const float t1min = __builtin_fminf(__builtin_fminf(t10, t11), t12);
         const float t0max = __builtin_fmaxf(__builtin_fmaxf(t00, t01), t02);
         // hit_cond = te > ts && t1min > ts && t0max < te && qa_i != qb_i (i.e. t1_i > t0_i) for
-        // every axis.  All six are strict orderings x > y of non-NaN values (te may be +inf), and
+        // every axis.  All six are strict orderings x > y of non-NaN values (te may be +inf): the
+        // quotients are finite, since upload bounds every node coordinate, leaf offset and the
+        // camera by 2^30 (rtw_world_upload: "node bounds beyond 2^30"), so |a_i| <= 2^31 and
+        // |q| <= 2^91 on this path's |d| >= 2^-60; no inf - inf arises.  And
         // for those x > y <=> RN(x - y) > 0 (no difference of distinct floats rounds to zero;
         // inf - finite = inf): one min over the six differences and one compare, instead of six
         // compares whose masks the scalar unit would AND together.
@@ -1785,6 +1788,40 @@ __global__ void accumulate_planes_kernel(const float* __restrict__ colors, uint3
     o[2] = r.z;
 }
 
+// The same merge when the whole frame's samples are in one launch: each plane is summed and divided
+// straight from the colour buffer, the last plane first (planes.pop()), then planes 0..n-2 are added
+// in order, so no plane buffer is needed (thread_count up to spp costs no memory beyond the colours).
+// Bit-identical to accumulate_planes_kernel: the same sums, divisions and merge order.
+__global__ void merge_planes_direct_kernel(const float* __restrict__ colors, uint32_t total, uint32_t n_planes,
+                                           uint32_t whole, uint32_t rem, float* out, int layout, int32_t width,
+                                           int32_t height, int32_t tile_w, int32_t tile_h, int32_t tiles_x,
+                                           int32_t part_index, int32_t part_count) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= total) return;
+    const int32_t per_tile = tile_w * tile_h;
+    const int32_t tile = part_index + (int32_t)(slot / (uint32_t)per_tile) * part_count;
+    const int32_t it = (int32_t)(slot % (uint32_t)per_tile);
+    const int32_t px = (tile % tiles_x) * tile_w + it % tile_w;
+    const int32_t py = (tile / tiles_x) * tile_h + it / tile_w;
+    if (px >= width || py >= height) return;  // padding slot of an edge tile
+    const size_t pstride = 3 * (size_t)total;
+    auto plane = [&](uint32_t t) {
+        const uint32_t n_t = whole + (t < rem ? 1u : 0u);
+        const uint32_t a = t * whole + min(t, rem);
+        V3 sum = v3(0.0f, 0.0f, 0.0f);
+        const float* c = colors + (size_t)a * pstride + 3 * (size_t)slot;
+        for (uint32_t s = 0; s < n_t; ++s, c += pstride) sum = add(sum, v3(c[0], c[1], c[2]));
+        return divs(sum, (float)n_t);
+    };
+    V3 r = plane(n_planes - 1);  // planes.pop()
+    for (uint32_t t = 0; t + 1 < n_planes; ++t) r = add(r, plane(t));
+    r = mul(r, 1.0f / (float)n_planes);
+    float* o = (layout == RTW_LAYOUT_TILES) ? out + 3 * (size_t)slot : out + 3 * ((size_t)py * width + px);
+    o[0] = r.x;
+    o[1] = r.y;
+    o[2] = r.z;
+}
+
 // per local tile: the summed slot costs (keys of the next frame's work order, saturated to 32 bits)
 // and its index; the slot costs then decay by half, so the order follows the recent frames (a
 // changed seed or camera re-weights within a few frames) and the per-slot counters stay bounded
@@ -2651,21 +2688,28 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
             budget = std::min<size_t>((size_t)64 << 30, std::max<size_t>((size_t)1 << 30, (free_b + g->colors_bytes) / 2));
     }
     const size_t per_sample = (size_t)A.total * 3 * sizeof(float);
-    uint64_t per_launch = std::max<uint64_t>(chunk, (budget / per_sample) / chunk * chunk);
-    per_launch = std::min<uint64_t>(per_launch, A.spp);
-    // the kernel decodes work items in 32 bits: keep a launch's items (plus a wave's overrun of
-    // the queue) below 2^32
-    per_launch = std::min<uint64_t>(per_launch, std::max<uint64_t>(chunk, ((0xFFFFFFFFull >> 1) / A.total) / chunk * chunk));
-    int rc = grow((void**)&g->colors, &g->colors_bytes, per_sample * per_launch);
-    if (rc != RTW_OK) return rc;
     // split_work_tasks (rendering.rs:222-237): planes of spp / T samples, the first spp % T one more
     const uint32_t T = (uint32_t)std::max(1, A.thread_count);
     const uint32_t whole = A.spp / T, rem = A.spp % T;
     const uint32_t n_planes = whole > 0 ? T : rem;
-    if (n_planes > 1) {
+    // the kernel decodes work items in 32 bits: keep a launch's items (plus a wave's overrun of
+    // the queue) below 2^32
+    const uint64_t item_cap = std::max<uint64_t>(chunk, ((0xFFFFFFFFull >> 1) / A.total) / chunk * chunk);
+    auto launch_samples = [&](size_t bytes) {
+        uint64_t n = std::max<uint64_t>(chunk, (bytes / per_sample) / chunk * chunk);
+        return std::min<uint64_t>(std::min<uint64_t>(n, A.spp), item_cap);
+    };
+    uint64_t per_launch = launch_samples(budget);
+    // More than one launch with planes: the plane partials live between launches, so their bytes
+    // come out of the budget first.  One launch merges straight from the colours (no plane buffer).
+    const bool plane_buffer = n_planes > 1 && per_launch < A.spp;
+    if (plane_buffer) per_launch = launch_samples(budget > per_sample * n_planes ? budget - per_sample * n_planes : 0);
+    int rc = grow((void**)&g->colors, &g->colors_bytes, per_sample * per_launch);
+    if (rc != RTW_OK) return rc;
+    if (plane_buffer) {
         rc = grow((void**)&g->running, &g->running_bytes, per_sample * n_planes);
         if (rc != RTW_OK) return rc;
-    } else if (per_launch < A.spp) {
+    } else if (n_planes <= 1 && per_launch < A.spp) {
         rc = grow((void**)&g->running, &g->running_bytes, per_sample);
         if (rc != RTW_OK) return rc;
     }
@@ -2725,7 +2769,11 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
         rc = launch_render(g, A, stats ? LK_STATS : LK_RENDER, stream);
         if (rc != RTW_OK) return rc;
         const unsigned blocks = (A.total + 255) / 256;
-        if (n_planes > 1)
+        if (n_planes > 1 && !plane_buffer)
+            hipLaunchKernelGGL(merge_planes_direct_kernel, dim3(blocks), dim3(256), 0, stream, (const float*)g->colors,
+                               A.total, n_planes, whole, rem, out, A.layout, A.width, A.height, A.tile_w, A.tile_h,
+                               A.tiles_x, A.part_index, A.part_count);
+        else if (n_planes > 1)
             hipLaunchKernelGGL(accumulate_planes_kernel, dim3(blocks), dim3(256), 0, stream, (const float*)g->colors, s0,
                                s1, A.total, g->running, n_planes, whole, rem, s1 == A.spp ? 1 : 0, out, A.layout,
                                A.width, A.height, A.tile_w, A.tile_h, A.tiles_x, A.part_index, A.part_count);

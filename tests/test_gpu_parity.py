@@ -268,11 +268,14 @@ def test_cost_ordered_frames_are_bit_identical(worlds, name, parts, buffer_bytes
 
 
 @pytest.mark.parametrize("threads,spp,buffer_bytes", [(1, 16, 0), (3, 16, 0), (16, 16, 0), (16, 5, 0), (3, 37, 40 * 24 * 12 * 5),
-                                                      (7, 37, 40 * 24 * 12 * 8)])
+                                                      (7, 37, 40 * 24 * 12 * 8), (64, 37, 0), (1000, 16, 0),
+                                                      (64, 37, 40 * 24 * 12 * 40)])
 def test_thread_count_planes_bit_exact(worlds, threads, spp, buffer_bytes, monkeypatch):
     """thread_count > 1: the device accumulation reproduces split_work_tasks + merge_planes
     (rendering.rs:222-252) bit for bit against the oracle's ctr-mode plane merge (itself checked
-    against a numpy restatement in tests/test_planes.py), also when the planes span launches."""
+    against a numpy restatement in tests/test_planes.py): merged straight from the colours in one
+    launch (no plane buffer, also for thread_count > spp), and with plane partials carried across
+    launches (the plane buffer's bytes taken out of RTW_SAMPLE_BUFFER_BYTES first)."""
     if buffer_bytes:
         monkeypatch.setenv("RTW_SAMPLE_BUFFER_BYTES", str(buffer_bytes))
     world = worlds("final_scene1")
