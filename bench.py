@@ -12,8 +12,13 @@ Extra fields:
                 benchmark) / the frame's render-launch time measured live with HIP events on the
                 launch stream, against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
                 instruction (MI355X_MICROARCH.md).  Also: VALU lane utilisation, effective clock,
-                the SURVEY §8(d) algorithmic-bytes rate (`effective_GBps`: node / primitive
-                records served from LDS and L2, not HBM) and the measured HBM `traffic`.
+                the measured HBM `traffic` (and its rate against the HBM peak), and `records`: the
+                SURVEY §8(d) record bytes of the traversal the timed kernel runs (its counting
+                variant: the SAH walk on SAH worlds) / kernel time, against the LDS peak -- the
+                node and primitive records are served from LDS (and L2), not HBM.
+  thread_count  the reference's own call shape: render(.., thread_count = available_parallelism,
+                ..) as main.rs:19 calls it (the plane split of rendering.rs:222-252 on the device),
+                N = 1 only, against the headline's thread_count 1.
   cpu_baseline  the C restatement of the reference render loop (oracle/) in the reference's own
                 scheme (ref mode: per-thread xoroshiro streams, split_work_tasks + merge_planes,
                 rendering.rs:121-252) on all of this host's CPUs (nproc), N = 1 only: the
@@ -38,6 +43,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+LDS_BYTES_PER_CLK = 256  # per CU: the LDS array is 64 dwords wide per clock (MI355X_MICROARCH.md §LDS)
 CLOCK_GHZ = 2.4        # MI355X peak engine clock (MI355X_MICROARCH.md)
 SIMDS_PER_CU = 4       # SIMD-32 units per CU; a wave64 VALU instruction issues over 2 cycles
 VALU_COUNTERS = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVE_CYCLES",
@@ -74,7 +80,8 @@ def _pmc_pass(args, counters) -> dict | None:
         return None
     child = [sys.executable, os.path.abspath(__file__), "--scene", args.scene, "--width", str(args.width), "--height",
              str(args.height), "--spp", str(args.spp), "--max-depth", str(args.max_depth), "--seed", str(args.seed),
-             "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-stats", "--no-pmc", "--no-first-frame"]
+             "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-stats", "--no-pmc", "--no-first-frame",
+             "--no-thread-count"]
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
         cmd = ["rocprofv3", "--pmc", *counters, "-d", d, "-o", "pmc", "--output-format", "csv", "--"] + child
         try:
@@ -242,6 +249,8 @@ def main() -> int:
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes (VALU counters, HBM traffic)")
     ap.add_argument("--no-traffic", action="store_true", help="skip only the HBM traffic passes")
     ap.add_argument("--no-first-frame", action="store_true")
+    ap.add_argument("--no-thread-count", action="store_true", help="skip the thread_count = available_parallelism leg")
+    ap.add_argument("--thread-count-leg", type=int, default=0, help="thread_count of that leg (0: available_parallelism)")
     ap.add_argument("--stats-spp", type=int, default=128, help="spp of the counting render (scaled to --spp)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -322,19 +331,25 @@ def main() -> int:
                 "peak_basis": f"{cus} CUs x {SIMDS_PER_CU} SIMD-32 x {CLOCK_GHZ} GHz / 2 cycles per wave64 VALU instruction"}
     if not args.no_stats:
         # the counting variant is ~8x slower than the product kernel: count at a bounded spp and
-        # scale to the frame's (per-sample counts do not depend on spp; samples are independent)
+        # scale to the frame's (per-sample counts do not depend on spp; samples are independent).
+        # tree 1: the traversal the timed kernel runs (the SAH walk + proofs + re-traces on SAH worlds)
         sp = type(fr.params).from_buffer_copy(fr.params)
         sp.samples_per_pixel = min(args.spp, args.stats_spp)
-        stats = fr.dworld.collect_stats(sp)
+        stats = fr.dworld.collect_stats(sp, tree=1)
         scale = args.spp / sp.samples_per_pixel
         stats = {k: int(round(v * scale)) for k, v in stats.items()}
         b = alg_bytes(stats, pix)
-        roofline["effective_GBps"] = round(b / (kernel_ms * 1e-3) / 1e9, 1)
-        roofline["effective_note"] = ("SURVEY §8(d) algorithmic record bytes / kernel time: node and primitive records "
-                                      "come from LDS and L2, so this is not HBM bandwidth (see traffic)")
-        roofline["alg_bytes_per_launch"] = b
-        roofline["counts"] = f"counting variant at {sp.samples_per_pixel} spp, scaled x{scale:g}"
-        roofline["per_sample"] = {k: round(v / max(1, stats["samples"]), 3) for k, v in stats.items() if k != "samples"}
+        lds_peak = cus * LDS_BYTES_PER_CLK * CLOCK_GHZ  # GB/s
+        rate = b / (kernel_ms * 1e-3) / 1e9
+        roofline["records"] = {
+            "bytes_per_launch": b, "GBps": round(rate, 1), "lds_peak_GBps": round(lds_peak, 1),
+            "lds_frac": round(rate / lds_peak, 4), "tree": fr.dworld.kernel_variant()["tree"],
+            "counts": f"counting variant of the timed kernel's traversal at {sp.samples_per_pixel} spp, scaled x{scale:g}",
+            "note": "SURVEY §8(d) record bytes (32 B per node or leaf-box visit, the primitive records, material and "
+                    "texel reads, the framebuffer) / kernel time; the records come from LDS and L2, so they are "
+                    "priced against the LDS array peak (256 B/clk/CU), not HBM (HBM: see traffic)",
+            "per_sample": {k: round(v / max(1, stats["samples"]), 3) for k, v in stats.items() if k != "samples"},
+        }
 
     if rank == 0 and world_size == 1 and not args.no_pmc:
         v = pmc_valu(args)
@@ -364,6 +379,34 @@ def main() -> int:
                     "fetch_bytes_x2": round(t["fetch_bytes"]), "write_bytes": round(t["write_bytes"]),
                     "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), the timed frame's "
                               f"render_kernel launches ({t['launches']})"}
+
+    tc_leg = None
+    if rank == 0 and world_size == 1 and not args.no_thread_count:
+        # main.rs:19: thread_count = available_parallelism() (the CPUs this process may use, as Rust
+        # reads them: affinity capped by the cgroup quota)
+        info = _cpu_info()
+        T = info["affinity"]
+        if info["cgroup_quota_cpus"]:
+            T = min(T, max(1, int(info["cgroup_quota_cpus"] + 0.5)))
+        T = args.thread_count_leg or T
+        spec_t = FrameSpec(spec.size, args.spp, args.max_depth, args.seed, thread_count=T)
+        fr_t = FrameRenderer(world, spec_t, 0, 1, local_rank)
+        fr_t.render_frame()  # warm-up (tuning, cost order)
+        barrier()
+        st_, en_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t = time.perf_counter()
+        st_.record()
+        for _ in range(2):
+            fr_t.launch()
+        en_.record()
+        barrier()
+        dt = (time.perf_counter() - t) / 2
+        tc_leg = {"thread_count": T, "value": round(args.width * args.height * args.spp / dt / 1e6, 3),
+                  "ms_per_step": round(dt * 1e3, 3), "kernel_ms": round(st_.elapsed_time(en_) / 2, 3),
+                  "vs_thread_count_1": round(elapsed / args.steps / dt, 4),
+                  "note": "render(.., thread_count, ..) as main.rs:19 calls it: split_work_tasks planes merged "
+                          "as merge_planes (rendering.rs:222-252) on the device; 2 frames after a warm-up"}
+        del fr_t
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -402,7 +445,10 @@ def main() -> int:
                 "kernel": fr.dworld.kernel_variant(),
             },
             "first_frame_ms": first_frame_ms,
+            "first_frame_Msamples_s": round(args.width * args.height * args.spp / first_frame_ms / 1e3, 1)
+            if first_frame_ms else None,
             "roofline": roofline,
+            "thread_count_leg": tc_leg,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

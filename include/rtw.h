@@ -279,9 +279,15 @@ RTW_API int rtw_partition_floats(const rtw_render_params* params, int64_t* float
  * image on the device (rank 0 after the RCCL gather). */
 RTW_API int rtw_untile_device(const rtw_render_params* params, const float* d_tiles,
                               int64_t stride_floats, float* d_image, void* stream);
-/* Synchronous statistics render (counting variant of the kernel). */
+/* Synchronous statistics render (counting variant of the kernel): the reference's traversal
+ * (hittable.rs:429-473 DFS over the reference BVH, with the proximity cull). */
 RTW_API int rtw_render_collect_stats(rtw_gpu_world* gw, const rtw_render_params* params,
                                      rtw_render_stats* stats);
+/* The same counts for the traversal the product kernel runs (tree 1): on worlds that take the SAH
+ * walk, its node and leaf visits plus the leaf-box proof and the re-traced rays; elsewhere as
+ * tree 0 (= rtw_render_collect_stats).  No reference counterpart: feeds the measured record bytes. */
+RTW_API int rtw_render_collect_stats_tree(rtw_gpu_world* gw, const rtw_render_params* params, int tree,
+                                          rtw_render_stats* stats);
 /* Profiling aid (no reference counterpart): the statistics render plus up to n wave-level
  * execution counters of the kernel, in this order: traversal calls, traversal loop iterations,
  * iterations that ran the node step, iterations that ran the leaf step, lane node steps, lane

@@ -247,6 +247,7 @@ _SIGS = {
     "rtw_partition_floats": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int64)]),
     "rtw_untile_device": (C.c_int, [C.POINTER(RenderParams), _P, C.c_int64, _P, _P]),
     "rtw_render_collect_stats": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(RenderStats)]),
+    "rtw_render_collect_stats_tree": (C.c_int, [_P, C.POINTER(RenderParams), C.c_int, C.POINTER(RenderStats)]),
     "rtw_render_progress": (C.c_int, [C.POINTER(World), C.POINTER(RenderParams), C.c_int, C.POINTER(C.c_float),
                                       _P, _P]),
     "rtw_render_debug_counters": (

@@ -42,11 +42,33 @@
 #define RTW_WAVE_BATCH 64  // work items a wave reserves per global atomic (upper bound)
 #endif
 #ifndef RTW_WAVE_BATCH_BIG
-#define RTW_WAVE_BATCH_BIG 256  // the same past the costly prefix of a cost-ordered launch
+#define RTW_WAVE_BATCH_BIG 1024  // the same past the first items of a launch (the costly tiles in cost order)
 #endif
 #ifndef RTW_BIG_BATCH_FROM
-#define RTW_BIG_BATCH_FROM 250  // that prefix, per mille of the launch's items (env overrides)
+#define RTW_BIG_BATCH_FROM 100  // that prefix, per mille of the launch's items (env overrides)
 #endif
+// The launch's work items are spread over RTW_QUEUES counters 256 B apart: queue q owns the
+// granules of RTW_QGRAN consecutive items whose index is q mod RTW_QUEUES, and a wave draws from
+// its own queue, moving on to the next one when that is empty.  Every queue walks the launch's
+// order (chunk-major or cost order) at the same pace.  One counter served every wave's refill
+// batch: a device-scope atomic on one address was the frame's limiter at 64-item batches (final_scene1
+// +10 % with 1024-item batches, which in turn let costly tiles pile up in one wave's reserve).
+#ifndef RTW_QUEUES
+#define RTW_QUEUES 16
+#endif
+#ifndef RTW_PREFETCH
+// 1: fetch a wave's next batch one refill ahead.  Measured slower (final_scene1 -3 %, suzanne -9 %,
+// profiles/r03/v1_queue_ab.txt): the pending atomic holds back the wave's next vector-memory waits
+// and a wave holds two batches; so the batch is fetched when the reserve runs out
+#define RTW_PREFETCH 0
+#endif
+#define RTW_QGRAN 64
+#define RTW_QSTRIDE 32  // u64 counters per queue slot (256 B)
+// a frame's launch l takes its items from queue block min(l, RTW_QUEUE_SLOTS - 1) of the world's
+// counters, so a progress poller can read how many items each launch has handed out
+#define RTW_QUEUE_SLOTS 32
+#define RTW_QUEUE_BLOCK (RTW_QUEUES * RTW_QSTRIDE)  // u64 per launch slot
+#define RTW_QUEUE_BYTES ((size_t)RTW_QUEUE_SLOTS * RTW_QUEUE_BLOCK * sizeof(unsigned long long))
 #ifndef RTW_BATCH_SPREAD
 #define RTW_BATCH_SPREAD 8  // a batch is at most 1/(SPREAD x waves) of the launch's remaining items
 #endif
@@ -81,7 +103,8 @@ struct DWorld {
     const int* perlin_bits;
     const struct WorldConst* wc; // camera / light / background, read from memory when used
     // the kernel's own search tree (rtw_sah.cpp; node format of node_a / node_b) and each leaf's
-    // Aabb (2 per leaf: {min.xyz, max.x}, {max.y, max.z, 0, 0}) for the verification (§5.6)
+    // proof box, its parent node's box in the reference tree (2 per leaf: {min.xyz, max.x},
+    // {max.y, max.z, 0, 0}), for the verification (§5.5)
     const float4* sah_a;
     const float4* sah_b;
     const float2* sah_km;
@@ -162,6 +185,7 @@ struct KArgs {
     uint32_t s_split;
     uint64_t items_big;  // items of the chunked range
     uint64_t items;
+    uint64_t q_cap;      // local items per queue: ceil(granules / RTW_QUEUES) * RTW_QGRAN
     float* colors;
     int32_t trace_min;       // dynamic ray fetch threshold (lanes still tracing), exit mode 0
     const DWorld* wdev;      // a copy of `w` in device memory (for the out-of-line shader)
@@ -172,6 +196,7 @@ struct KArgs {
     unsigned long long* stats; // 13 counters (stats variant only)
     TuneState* tune;          // in-frame threshold tuning, or null
     int32_t mk_world;         // node coordinates admit the per-ray exact-division guard (ray_pre)
+    int32_t stats_tree;       // counting variant: 0 the reference tree, 1 the tree the product kernel walks
     int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
                               // re-traced on the reference tree where the proof does not hold (§5.6)
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
@@ -403,15 +428,20 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
     return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 // the per-ray part; barycentrics are recomputed from (ray, t) by leaf_record
+#ifdef RTW_EXP_FASTDIV_TRI  // experiment builds only (inexact: wrong images): the cost of the divisions
+#define RTW_TDIV(a, b) ((a) * __builtin_amdgcn_rcpf(b))
+#else
+#define RTW_TDIV(a, b) ((a) / (b))
+#endif
 __device__ __forceinline__ bool tri_test(const TriFast& T, const Ray& r, float ts, float te, float& t) {
     const float denom = dot(r.d, T.n);
     if (!(__builtin_fabsf(denom) > 0.0001f)) return false;
-    t = dot(sub(T.p0, r.o), T.n) / denom;
+    t = RTW_TDIV(dot(sub(T.p0, r.o), T.n), denom);
     if (!contains(ts, te, t)) return false;
     const V3 q = sub(at(r, t), T.p0);
-    const float w1 = dot(q, T.vt1) / T.den1;
+    const float w1 = RTW_TDIV(dot(q, T.vt1), T.den1);
     if (!(w1 > 0.0f && w1 < 1.0f)) return false;
-    const float w2 = dot(q, T.vt2) / T.den2;
+    const float w2 = RTW_TDIV(dot(q, T.vt2), T.den2);
     const float w0 = 1.0f - w1 - w2;
     return w2 > 0.0f && w0 > 0.0f;
 }
@@ -1293,6 +1323,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             const float4 la = nodes_a[il], lb = nodes_b[il], ra = nodes_a[ir], rb = nodes_b[ir];
             const float2 lk = nkm[il], rk = nkm[ir];
             float el, er;
+            if (STATS) st.c[ST_NODES] += (left >= 0) + (right >= 0);  // the child boxes tested
             const bool pl = node_pass_cons(la, lb, lk, T.ray, rp, 0.001f, T.te, el) || left < 0;
             const bool pr = node_pass_cons(ra, rb, rk, T.ray, rp, 0.001f, T.te, er) || right < 0;
             if (left < 0) el = -F32_INF;
@@ -1352,9 +1383,9 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
     // per node)] [stack: depth x BLOCK]
     const DWorld& w = A.w;
-    // SAH path (§5.6): worlds of plain spheres / triangles only, never in the counting variant
-    // (whose statistics are the reference traversal's)
-    constexpr bool SAHK = !STATS && LK <= LK_TRIS;
+    // SAH path (§5.6): worlds of plain spheres / triangles only; in the counting variant only when
+    // asked for the product kernel's own traversal (stats_tree 1; else the reference's statistics)
+    constexpr bool SAHK = LK <= LK_WRAPPED;
     const bool sah = SAHK && A.sah != 0;
     if (LDS_SCENE) {
         const float4* ga = sah ? w.sah_a : w.node_a;
@@ -1426,11 +1457,25 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         if (ch > 0) trace_min = ch;
         else tuned = A.tune_items == 0;
     }
-    // This wave's reserve of work items [w_next, w_end), taken from the launch's counter in batches
-    // (one global atomic per batch instead of per refill round: a single counter hit by every
-    // wave's refills throttled fast-sample worlds); batches shrink toward the end of the launch so
-    // that the last items still spread over all waves.
+    // This wave's reserve of work items [w_next, w_end), in the local index space of its queue wq,
+    // taken from the queue's counter in batches (one global atomic per batch, not per refill round);
+    // batches shrink toward the end of the launch so that the last items still spread over all
+    // waves.  (RTW_PREFETCH 1 fetches the next batch one refill ahead instead.)
     uint64_t w_next = 0, w_end = 0;
+    uint32_t wq = (blockIdx.x * (RTW_BLOCK / 64) + (threadIdx.x >> 6)) % RTW_QUEUES;
+    uint32_t qfail = 0;           // consecutive queues found empty: RTW_QUEUES of them end the launch
+    unsigned long long pf_b = 0;  // the prefetched batch's base, in lane pf_lane (its atomic's result)
+    uint64_t pf_size = 0;         // its size; 0: none in flight
+    int pf_lane = 0;
+    auto prefetch = [&](int leader) {  // wave-uniform
+        const uint64_t rest = A.q_cap > w_end ? A.q_cap - w_end : 0;
+        // small batches while the costly tiles are handed out: a wave slowed by long paths must not
+        // sit on a large reserve of them (an 8-GPU suzanne rank: 2.4x at 256)
+        const uint64_t cap = w_end * RTW_QUEUES >= A.big_from ? RTW_WAVE_BATCH_BIG : RTW_WAVE_BATCH;
+        pf_size = max((uint64_t)1, min(cap, (uint64_t)fdiv((uint32_t)rest, A.fd_spread)));
+        if (lane == leader) pf_b = atomicAdd(A.queue + wq * RTW_QSTRIDE, (unsigned long long)pf_size);
+        pf_lane = leader;
+    };
     RTW_PT_DECL
     for (;;) {
         // 1. lanes without a pixel take the next items of the wave's reserve
@@ -1439,33 +1484,49 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         for (;;) {
             const unsigned long long m = __ballot(T.phase == PH_PIXEL);
             if (m == 0) break;
+            if (qfail >= RTW_QUEUES) {  // wave-uniform: every queue is empty
+#ifdef RTW_WAVE_TIMING
+                {
+                    const uint32_t wv_ = (blockIdx.x * RTW_BLOCK + threadIdx.x) / 64;
+                    if (wv_ < 8192) atomicMin(&rtw_wave_dry[wv_], (unsigned long long)wall_clock64());
+                }
+#endif
+                if (T.phase == PH_PIXEL) {
+                    out_of_work = true;
+                    T.phase = PH_TRACE;  // leaves the loops below
+                }
+                continue;
+            }
             const int leader = __ffsll((long long)m) - 1;
             const uint64_t need = (uint64_t)__popcll(m);
-            // the first `left` lanes take the reserve's rest, the others a new batch from `base`
-            const uint64_t left = min(need, w_end - w_next);
-            uint64_t base = w_end;
-            if (left < need) {
-                const uint64_t rest = A.items > w_end ? A.items - w_end : 0;
-                // small batches while the costly tiles are handed out: a wave slowed by long paths
-                // must not sit on a large reserve of them (an 8-GPU suzanne rank: 2.4x at 256)
-                const uint64_t cap = w_end >= A.big_from ? RTW_WAVE_BATCH_BIG : RTW_WAVE_BATCH;
-                const uint64_t batch = max(need - left, min(cap, (uint64_t)fdiv((uint32_t)rest, A.fd_spread)));
-                unsigned long long b = 0;
-                if (lane == leader) b = atomicAdd(A.queue, (unsigned long long)batch);
-                base = __shfl(b, leader);
-                if (!tuned) {  // wave-uniform; the batch holding a half-epoch's first item stamps its start
+            bool empty = false, took = false;
+            if (w_next == w_end) {  // reserve used up: take the prefetched batch (fetch one if none)
+                if (pf_size == 0) prefetch(leader);
+                const uint64_t base =
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pf_b >> 32), pf_lane) << 32) |
+                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pf_b, pf_lane);
+                const uint64_t size = pf_size;
+                pf_size = 0;
+                took = true;
+                empty = base >= A.q_cap;
+                w_next = empty ? A.q_cap : base;
+                w_end = empty ? A.q_cap : min(base + size, A.q_cap);
+                if (!tuned && wq == 0 && !empty) {  // wave-uniform; queue 0's batch holding a half-epoch's
+                    // first item (global position ~ local x RTW_QUEUES) stamps its start
                     const uint64_t H = A.fd_half.d;
-                    const uint64_t j = fdiv((uint32_t)(base + H - 1), A.fd_half);
-                    if (lane == leader && j >= 1 && j <= RTW_TUNE_STAMPS && j * H < base + batch)
+                    const uint64_t g0 = base * RTW_QUEUES, g1 = (base + size) * RTW_QUEUES;
+                    const uint64_t j = fdiv((uint32_t)min(g0 + H - 1, (uint64_t)0xFFFFFFFFu), A.fd_half);
+                    if (lane == leader && j >= 1 && j <= RTW_TUNE_STAMPS && j * H < g1)
                         __hip_atomic_store(&A.tune->tb[j - 1], wall_clock64(), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
-                w_end = base + batch;
+                if (!empty && RTW_PREFETCH) prefetch(leader);  // the next batch, in flight while this one is used
             }
+            const uint64_t left = min(need, w_end - w_next);  // the first `left` lanes get an item
             const uint64_t first = w_next;
-            w_next = (left < need) ? base + (need - left) : w_next + need;
+            w_next += left;
             if (!tuned) {  // wave-uniform: the epoch of the items being handed out
-                const uint64_t e = fdiv((uint32_t)w_next, A.fd_epoch);
+                const uint64_t e = fdiv((uint32_t)min(w_next * RTW_QUEUES, (uint64_t)0xFFFFFFFFu), A.fd_epoch);
                 if (e == 0) {
                     trace_min = A.trace_min;
                 } else if (e <= RTW_TUNE_EPOCHS) {
@@ -1504,16 +1565,12 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             if (T.phase == PH_PIXEL) {
                 const unsigned long long below = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
                 const uint64_t r = (uint64_t)__popcll(below);
-                const uint64_t item = r < left ? first + r : base + (r - left);
-                if (item >= A.items) {
-#ifdef RTW_WAVE_TIMING
-                    {
-                        const uint32_t wv_ = (blockIdx.x * RTW_BLOCK + threadIdx.x) / 64;
-                        if (wv_ < 8192) atomicMin(&rtw_wave_dry[wv_], (unsigned long long)wall_clock64());
-                    }
-#endif
-                    out_of_work = true;
-                    T.phase = PH_TRACE;  // leaves the loops below
+                const uint64_t loc = first + r;
+                // queue wq's local item -> the launch's item (granule loc / QGRAN of queue wq)
+                const uint64_t item = ((loc / RTW_QGRAN) * RTW_QUEUES + wq) * RTW_QGRAN + loc % RTW_QGRAN;
+                if (r >= left || item >= A.items) {
+                    // nothing for this lane in this round: the reserve is used up (the next round takes
+                    // the next batch) or a padding index of the last granule row
                 } else {
                     const bool big = item < A.items_big;
                     const uint32_t rel = (uint32_t)(big ? item : item - A.items_big);  // < 2^32
@@ -1546,6 +1603,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         T.phase = PH_TRACE;
                     }
                 }
+            }
+            if (empty) {  // wave-uniform: queue wq is used up (no batch in flight); try the next one
+                wq = (wq + 1) % RTW_QUEUES;
+                ++qfail;
+                w_next = w_end = 0;
+            } else if (took) {
+                qfail = 0;
             }
         }
         if (out_of_work) break;
@@ -1584,18 +1648,28 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         // path (wave-uniform choice per call)
         if (sah) {
             T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
-                                                       A.leaf_count, A.rect_count, A.tri_count, stack_off, nullptr);
-            // §5.6: the SAH walk's closest leaf L (no tie) is the reference's answer when the
-            // reference DFS reaches L: every ancestor box contains L's Aabb (checked at upload) and
-            // hit_cond is monotone under box inclusion and in te, so L's own box passing hit_cond
-            // with te = succ(t) proves it.  A miss is a miss for the reference too.  Otherwise the
-            // ray is traced again on the reference tree.
+                                                       A.leaf_count, A.rect_count, A.tri_count, stack_off,
+                                                       STATS ? A.stats + ST_COUNT : nullptr);
+            if (STATS) {
+                st.c[ST_NODES] += T.n_nodes;
+                st.c[ST_T_SPHERE] += T.n_sph_rect & 0xFFFFu;
+                st.c[ST_T_RECT] += T.n_sph_rect >> 16;
+                st.c[ST_T_BOX] += T.n_box_tri & 0xFFFFu;
+                st.c[ST_T_TRI] += T.n_box_tri >> 16;
+                T.n_nodes = T.n_sph_rect = T.n_box_tri = 0;
+            }
+            // §5.5: the SAH walk's closest leaf L (no tie) is the reference's answer when the
+            // reference DFS reaches L: the reference's internal boxes are nested (checked at upload)
+            // and hit_cond is monotone under box inclusion and in te, so L's parent box passing
+            // hit_cond with te = succ(t) proves it.  A miss is a miss for the reference too.
+            // Otherwise the ray is traced again on the reference tree.
             if (T.phase == PH_SHADE && (T.fast & RTW_TF_SAH)) {
                 bool ok = (T.fast & RTW_TF_TIE) == 0;
 #ifdef RTW_SAH_AUDIT_NO_TIE  // audit builds only: shows that the tie test decides images
                 ok = true;
 #endif
                 if (T.found >= 0) {
+                    if (STATS) st.c[ST_NODES]++;  // the leaf-box proof reads one 32-B box record
                     const float4 ba = w.leaf_box[2 * T.found], bb = w.leaf_box[2 * T.found + 1];
 #ifndef RTW_SAH_AUDIT_NO_BOX  // audit builds only: shows that the leaf-box proof decides images
                     ok = ok && box_hit_cond_fast(ba, bb, T.ray, RayPre{T.inv, true}, 0.001f, T.te);
@@ -1615,7 +1689,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             }
             if (__ballot(T.phase == PH_REF) != 0)
                 T = traverse<STATS, LDS, LK, false, TM_FALLBACK>(A.wdev, T, 0, A.node_count, A.leaf_count, A.rect_count,
-                                                                 A.tri_count, stack_off, nullptr);
+                                                                 A.tri_count, stack_off,
+                                                                 STATS ? A.stats + ST_COUNT : nullptr);
         } else if (__ballot(T.phase == PH_TRACE && (T.fast & 8) == 0) == 0) {
             T = traverse<STATS, LDS, LK, true>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
                                                A.leaf_count, A.rect_count, A.tri_count, stack_off,
@@ -2042,14 +2117,19 @@ int check_world(const rtw_world* w, int* depth_out) {
     return RTW_OK;
 }
 
-// The SAH path's tables (§5.6), or empty when the world does not qualify: every leaf a plain
-// sphere or triangle, the reference tree's boxes nested (each child's box -- a leaf's own Aabb,
-// aabb.rs new_radius / new_surrounding_points -- inside its parent's), every leaf-box coordinate
-// admitting the exact fast division (0 or >= 2^-60 in magnitude), and RTW_NO_SAH unset.
+// The SAH path's tables (§5.5), or empty when the world does not qualify: no volume leaves (their
+// RNG draws depend on the visit order), every leaf cullable with its true world box (rtw_cull_leaf,
+// wrapped = 1: plain or Transformation / Animation spheres, triangles, rects and boxes), every box
+// coordinate admitting the fast division (0 or 2^-60 .. 2^30 in magnitude), the reference tree's
+// internal boxes nested (each child node's box inside its parent's), and RTW_NO_SAH unset.
+// The proof box of a leaf (box_hit_cond_fast after the walk) is its parent node's box in the
+// reference tree: when it passes hit_cond at te = succ(t), so do all ancestors (nested, monotone),
+// and the reference DFS reaches the leaf -- whose own Aabb, for a wrapped leaf the apply_aabb
+// quirk's untransformed box, need not hold the hit at all.
 struct SahTables {
     std::vector<float4> a, b;     // nodes, as node_a / node_b
     std::vector<float> km;        // cull constants, 2 per node
-    std::vector<float4> box;      // 2 per leaf: the leaf's Aabb
+    std::vector<float4> box;      // 2 per leaf: the proof box (the leaf's parent box in the reference tree)
     int32_t root = 0, depth = 0;
     bool ok = false;
 };
@@ -2058,51 +2138,53 @@ SahTables build_sah_tables(const rtw_world* w) {
     if (const char* e = std::getenv("RTW_NO_SAH"))
         if (e[0] && e[0] != '0') return S;
     const int32_t L = w->leaf_count;
-    if (L < 2 || w->root < 0) return S;
+    if (L < 2 || w->root < 0 || w->node_count < 1) return S;
+    auto coord_ok = [](float c) { return c == 0.0f || (std::fabs(c) >= 0x1p-60f && std::fabs(c) <= 1073741824.0f); };
     std::vector<float> lo((size_t)L * 3), hi((size_t)L * 3);
+    std::vector<uint8_t> never((size_t)L, 0);
     for (int32_t i = 0; i < L; ++i) {
-        const rtw_leaf& l = w->leaves[i];
-        if (l.flags != 0) return S;
+        float k, m;
+        int nv = 0;
         float* mn = &lo[3 * (size_t)i];
         float* mx = &hi[3 * (size_t)i];
-        if (l.geom_kind == RTW_GEOM_SPHERE) {  // Aabb::new_radius: center -+ (r, r, r)
-            const rtw_sphere& sp = w->spheres[l.geom_index];
-            for (int k = 0; k < 3; ++k) {
-                mn[k] = sp.center[k] - sp.radius;
-                mx[k] = sp.center[k] + sp.radius;
+        if (!rtw_cull_leaf(w, &w->leaves[i], 1, &k, &m, mn, mx, &nv)) return S;
+        never[(size_t)i] = (uint8_t)nv;
+        if (nv) {  // a leaf that never reports a hit: any box (it only has to sit somewhere in the tree)
+            const rtw_triangle& t = w->triangles[w->leaves[i].geom_index];
+            for (int k2 = 0; k2 < 3; ++k2) {
+                mn[k2] = rtw_minr(rtw_minr(t.positions[0][k2], t.positions[1][k2]), t.positions[2][k2]);
+                mx[k2] = rtw_maxr(rtw_maxr(t.positions[0][k2], t.positions[1][k2]), t.positions[2][k2]);
             }
-        } else if (l.geom_kind == RTW_GEOM_TRIANGLE) {  // Aabb::new_surrounding_points
-            const rtw_triangle& t = w->triangles[l.geom_index];
-            for (int k = 0; k < 3; ++k) {
-                mn[k] = rtw_minr(rtw_minr(t.positions[0][k], t.positions[1][k]), t.positions[2][k]);
-                mx[k] = rtw_maxr(rtw_maxr(t.positions[0][k], t.positions[1][k]), t.positions[2][k]);
-            }
-        } else {
-            return S;
         }
-        for (int k = 0; k < 3; ++k)
-            for (float c : {mn[k], mx[k]})
-                if (!(c == 0.0f || (std::fabs(c) >= 0x1p-60f && std::fabs(c) <= 1073741824.0f))) return S;
+        for (int k2 = 0; k2 < 3; ++k2)
+            if (!coord_ok(mn[k2]) || !coord_ok(mx[k2])) return S;
     }
-    // nested reference boxes: then every ancestor of a leaf contains the leaf's Aabb
+    // nested reference boxes (internal children inside their parents) and each leaf's parent
+    std::vector<int32_t> parent((size_t)L, -1);
     for (int32_t n = 0; n < w->node_count; ++n) {
         const rtw_bvh_node& nd = w->nodes[n];
+        for (int k2 = 0; k2 < 3; ++k2)
+            if (!coord_ok(nd.min[k2]) || !coord_ok(nd.max[k2])) return S;
         for (int32_t c : {nd.left, nd.right}) {
-            const float* cmn = c >= 0 ? w->nodes[c].min : &lo[3 * (size_t)(-1 - c)];
-            const float* cmx = c >= 0 ? w->nodes[c].max : &hi[3 * (size_t)(-1 - c)];
-            for (int k = 0; k < 3; ++k)
-                if (!(nd.min[k] <= cmn[k] && cmx[k] <= nd.max[k])) return S;
+            if (c < 0) {
+                parent[(size_t)(-1 - c)] = n;
+                continue;
+            }
+            for (int k2 = 0; k2 < 3; ++k2)
+                if (!(nd.min[k2] <= w->nodes[c].min[k2] && w->nodes[c].max[k2] <= nd.max[k2])) return S;
         }
     }
+    for (int32_t i = 0; i < L; ++i)
+        if (parent[(size_t)i] < 0) return S;  // a leaf outside the reference tree
     std::vector<rtw_bvh_node> nodes;
     if (rtw::sah_build(lo.data(), hi.data(), L, nodes, &S.root, &S.depth) != 0 || S.depth > RTW_STACK) return S;
-    // cull constants of the SAH tree: the same per-leaf bounds, maximised over its subtrees
+    // cull constants of the SAH tree over the leaves' true world boxes (wrapped leaves included)
     rtw_world tw = *w;
     tw.nodes = nodes.data();
     tw.node_count = (int32_t)nodes.size();
     tw.root = S.root;
     S.km.assign(nodes.size() * 2, 0.0f);
-    rtw_cull_prepare(&tw, S.km.data(), 0);
+    rtw_cull_prepare_ex(&tw, S.km.data(), 0, 1);
     for (float& c : S.km)  // x17/16 rounded up (inf stays inf): the cheap quotients' slack, node_pass_cons
         if (c > 0.0f) c = std::nextafter(c * RTW_SAH_WIDEN, std::numeric_limits<float>::infinity());
     S.a.resize(nodes.size());
@@ -2114,10 +2196,9 @@ SahTables build_sah_tables(const rtw_world* w) {
     }
     S.box.resize((size_t)L * 2);
     for (int32_t i = 0; i < L; ++i) {
-        const float* mn = &lo[3 * (size_t)i];
-        const float* mx = &hi[3 * (size_t)i];
-        S.box[2 * (size_t)i] = make_float4(mn[0], mn[1], mn[2], mx[0]);
-        S.box[2 * (size_t)i + 1] = make_float4(mx[1], mx[2], 0.0f, 0.0f);
+        const rtw_bvh_node& p = w->nodes[parent[(size_t)i]];
+        S.box[2 * (size_t)i] = make_float4(p.min[0], p.min[1], p.min[2], p.max[0]);
+        S.box[2 * (size_t)i + 1] = make_float4(p.max[1], p.max[2], 0.0f, 0.0f);
     }
     S.ok = true;
     return S;
@@ -2440,7 +2521,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     }
     e = hipMalloc(&g->tune, sizeof(TuneState));
     if (e == hipSuccess) e = hipMemset(g->tune, 0, sizeof(TuneState));
-    if (e == hipSuccess) e = hipMalloc(&g->queue, 256);
+    if (e == hipSuccess) e = hipMalloc(&g->queue, RTW_QUEUE_BYTES);
     if (e != hipSuccess) {
         (void)hipFree(g->arena);
         delete g;
@@ -2526,6 +2607,7 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.queue = g->queue;
     A.wdev = g->wdev;
     A.trace_min = 32;
+    A.stats_tree = 0;
     if (const char* e = getenv("RTW_TRACE_MIN")) A.trace_min = atoi(e);
     A.seed_key = rtw_seed_key(p->seed);
     A.sx = 1.0f / (float)(p->width - 1);
@@ -2540,13 +2622,14 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
 enum LaunchKind { LK_RENDER, LK_STATS };
 int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const bool stats = kind == LK_STATS;
+    const bool ktree = stats && A.stats_tree == 1;  // count the product kernel's own traversal
     // the leaf and texture kinds the world needs; RTW_LEAF_KINDS=4 / RTW_TEX_KINDS=1 force the
     // generic code (audits)
     int lk = g->leaf_kinds, tx = g->tex_kinds;
     if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RTW_TEX_KINDS")) tx = std::max(tx, std::min(1, std::atoi(e)));
     // the SAH tree (§5.6) replaces the reference tree in LDS; the counting variant keeps the latter
-    const bool sah = !stats && g->sah_nodes > 0 && g->mk_world && lk <= LK_TRIS;
+    const bool sah = (!stats || ktree) && g->sah_nodes > 0 && g->mk_world && lk <= LK_WRAPPED;
     A.sah = sah ? 1 : 0;
     A.node_count = sah ? g->sah_nodes : g->node_count;
     const size_t scene_bytes =
@@ -2575,7 +2658,11 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
 #undef RTW_KSET
     static const KFn fns_stats[3] = {render_kernel<true, 0, LK_ANY, TX_ANY>, render_kernel<true, 1, LK_ANY, TX_ANY>,
                                      render_kernel<true, 2, LK_ANY, TX_ANY>};
-    const KFn kf = stats ? fns_stats[mode] : fns[tx][lk][mode];
+#define RTW_SSET(LK) {render_kernel<true, 0, LK, TX_ANY>, render_kernel<true, 1, LK, TX_ANY>, render_kernel<true, 2, LK, TX_ANY>}
+    static const KFn fns_stats_sah[4][3] = {RTW_SSET(LK_SPHERES), RTW_SSET(LK_TRIS), RTW_SSET(LK_PLAIN),
+                                            RTW_SSET(LK_WRAPPED)};
+#undef RTW_SSET
+    const KFn kf = stats ? (sah ? fns_stats_sah[lk][mode] : fns_stats[mode]) : fns[tx][lk][mode];
     if (!stats) {
         g->last_kernel[0] = mode;
         g->last_kernel[1] = lk;
@@ -2589,7 +2676,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     if (per_cu < 1) return rtw::fail(RTW_ERR_UNSUPPORTED, "render kernel does not fit on a CU");
     const int64_t want = (int64_t)((A.items + RTW_BLOCK - 1) / RTW_BLOCK);
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per_cu * g->cus));
-    HIP_TRY(hipMemsetAsync(A.queue, 0, sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(A.queue, 0, RTW_QUEUE_BLOCK * sizeof(unsigned long long), stream));
     // tuning epochs: whole passes over the slots, at least 2x the resident lanes in items (the
     // items in flight blur epoch boundaries; mirrored candidates cancel the blur's bias); explore
     // only if warm-up + all epochs + one more fit (a 1080p x 512 spp frame split over 8 GPUs does)
@@ -2602,7 +2689,8 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
             HIP_TRY(hipMemsetAsync(A.tune->tb, 0xFF, sizeof(A.tune->tb), stream));
         }
     }
-    A.fd_spread = fastdiv_make((uint32_t)(RTW_BATCH_SPREAD * blocks * (RTW_BLOCK / 64)));
+    // a queue's remaining items are shared by the waves drawing from it (1 / RTW_QUEUES of them)
+    A.fd_spread = fastdiv_make((uint32_t)std::max<int64_t>(1, RTW_BATCH_SPREAD * blocks * (RTW_BLOCK / 64) / RTW_QUEUES));
     A.fd_epoch = fastdiv_make((uint32_t)std::max<uint64_t>(1, A.tune_items));
     A.fd_half = fastdiv_make((uint32_t)std::max<uint64_t>(1, A.tune_items / 2));
     hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(RTW_BLOCK), lds, stream, A);
@@ -2621,6 +2709,12 @@ size_t env_size(const char* name, size_t dflt) {
     return v > 0 ? (size_t)v : dflt;
 }
 
+// local items per queue for a launch of `items` items (RTW_QUEUES, RTW_QGRAN)
+uint64_t queue_cap(uint64_t items) {
+    const uint64_t gran = (items + RTW_QGRAN - 1) / RTW_QGRAN;
+    return (gran + RTW_QUEUES - 1) / RTW_QUEUES * RTW_QGRAN;
+}
+
 void set_items(KArgs& A, uint32_t chunk) {
     const uint32_t n = A.s_end - A.s_begin;
     // chunk-major order drains on single-sample items; in cost order the cheapest tiles come last
@@ -2629,10 +2723,13 @@ void set_items(KArgs& A, uint32_t chunk) {
     A.s_split = A.s_end - tail;
     A.items_big = (uint64_t)A.total * ((A.s_split - A.s_begin + chunk - 1) / chunk);
     A.items = A.items_big + (uint64_t)A.total * tail;
+    A.q_cap = queue_cap(A.items);
     A.chunks = (A.s_split - A.s_begin + chunk - 1) / chunk;
-    // chunk-major launches keep small batches throughout; cost order after its costly prefix
-    A.big_from = A.tile_perm ? A.items / 1000 * std::min<size_t>(1000, env_size("RTW_BIG_BATCH_FROM", RTW_BIG_BATCH_FROM))
-                             : ~0ull;
+    // big batches after the first 10 % of the items: in cost order the costly tiles come first and a
+    // wave slowed by long paths must not sit on a big reserve of them (suzanne's 8-GPU shares: 74 ms
+    // at a 10 % prefix, 93-103 ms without one); each batch is a device-scope atomic whose round trip
+    // stalls the wave (final_scene1 +5.6 % with 1024 over 256, profiles/r03/v2_batch_sweep.txt)
+    A.big_from = A.items / 1000 * std::min<size_t>(1000, env_size("RTW_BIG_BATCH_FROM", RTW_BIG_BATCH_FROM));
     const uint32_t per_tile = (uint32_t)(A.tile_w * A.tile_h);
     A.fd_total = fastdiv_make(A.total);
     A.fd_tile = fastdiv_make(per_tile);
@@ -2655,9 +2752,8 @@ int grow(void** buf, size_t* have, size_t need) {
 // One frame: launches of at most RTW_SAMPLE_BUFFER_BYTES (default: half of the HBM this world could
 // use, at most 64 GiB) of per-sample colours,
 // each followed by the in-order accumulation; work items of RTW_CHUNK (default 8) samples.
-// Launch l of a frame takes its work items from counter min(l, RTW_QUEUE_SLOTS - 1) of the
-// world's queue block, so a progress poller can read how many items each launch has handed out.
-#define RTW_QUEUE_SLOTS 32
+// Launch l of a frame takes its work items from queue block min(l, RTW_QUEUE_SLOTS - 1) of the
+// world's counters, so a progress poller can read how many items each launch has handed out.
 int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream,
                       std::vector<uint64_t>* launch_items);
 
@@ -2757,14 +2853,14 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
         A.slot_cost = g->slot_cost;
         if (g->order_valid) A.tile_perm = g->tile_buf + 3 * (size_t)n_tiles_local;
     }
-    HIP_TRY(hipMemsetAsync(g->queue, 0, RTW_QUEUE_SLOTS * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(g->queue, 0, RTW_QUEUE_BYTES, stream));
     int launch = 0;
     for (uint32_t s0 = 0; s0 < A.spp; s0 += (uint32_t)per_launch, ++launch) {
         const uint32_t s1 = (uint32_t)std::min<uint64_t>(A.spp, s0 + per_launch);
         A.s_begin = s0;
         A.s_end = s1;
         set_items(A, chunk);
-        A.queue = g->queue + std::min(launch, RTW_QUEUE_SLOTS - 1);
+        A.queue = g->queue + (size_t)std::min(launch, RTW_QUEUE_SLOTS - 1) * RTW_QUEUE_BLOCK;
         if (launch_items) launch_items->push_back(A.items);
         rc = launch_render(g, A, stats ? LK_STATS : LK_RENDER, stream);
         if (rc != RTW_OK) return rc;
@@ -2822,10 +2918,12 @@ extern "C" RTW_API int rtw_render_device(rtw_gpu_world* g, const rtw_render_para
 }
 
 namespace {
-int collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s, uint64_t* dbg, int dbg_n) {
+int collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s, uint64_t* dbg, int dbg_n,
+                  int tree = 0) {
     KArgs A;
     const int v = make_args(g, p, A);
     if (v != RTW_OK) return v;
+    A.stats_tree = tree;
     if (!s) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null stats");
     HIP_TRY(hipSetDevice(g->device));
     float* out = nullptr;
@@ -2866,6 +2964,12 @@ int collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats
 
 extern "C" RTW_API int rtw_render_collect_stats(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s) {
     return collect_stats(g, p, s, nullptr, 0);
+}
+
+extern "C" RTW_API int rtw_render_collect_stats_tree(rtw_gpu_world* g, const rtw_render_params* p, int tree,
+                                                     rtw_render_stats* s) {
+    if (tree != 0 && tree != 1) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "tree must be 0 or 1");
+    return collect_stats(g, p, s, nullptr, 0, tree);
 }
 
 extern "C" RTW_API int rtw_render_debug_counters(rtw_gpu_world* g, const rtw_render_params* p, rtw_render_stats* s,
@@ -2923,7 +3027,7 @@ extern "C" RTW_API int rtw_render_progress(const rtw_world* w, const rtw_render_
     hipStream_t rs = nullptr, ps = nullptr;
     hipEvent_t fin = nullptr;
     hipError_t e = hipMalloc(&d, bytes);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&h, RTW_QUEUE_SLOTS * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h, RTW_QUEUE_BYTES);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&rs, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&fin, hipEventDisableTiming);
@@ -2947,11 +3051,16 @@ extern "C" RTW_API int rtw_render_progress(const rtw_world* w, const rtw_render_
                     e = qe;
                     break;
                 }
-                e = hipMemcpyAsync(h, g->queue, RTW_QUEUE_SLOTS * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                   ps);
+                e = hipMemcpyAsync(h, g->queue, RTW_QUEUE_BYTES, hipMemcpyDeviceToHost, ps);
                 if (e == hipSuccess) e = hipStreamSynchronize(ps);
-                uint64_t taken = 0;
-                for (size_t l = 0; l < items.size() && l < RTW_QUEUE_SLOTS; ++l) taken += std::min<uint64_t>(h[l], items[l]);
+                uint64_t taken = 0;  // local items handed out, over the launch's queues (padding included)
+                for (size_t l = 0; l < items.size() && l < RTW_QUEUE_SLOTS; ++l) {
+                    const uint64_t cap = queue_cap(items[l]);
+                    uint64_t t = 0;
+                    for (int q = 0; q < RTW_QUEUES; ++q)
+                        t += std::min<uint64_t>(h[l * RTW_QUEUE_BLOCK + q * RTW_QSTRIDE], cap);
+                    taken += std::min<uint64_t>(t, items[l]);
+                }
                 const uint64_t done = all ? (uint64_t)((double)total * (double)taken / (double)all) : 0;
                 if (e == hipSuccess && done != last && done < total) {
                     cb(done, total, user);

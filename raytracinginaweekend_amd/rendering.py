@@ -132,9 +132,15 @@ class DeviceWorld:
         return {"lds_mode": m.value, "leaf_kinds": lk.value, "tex_kinds": tx.value,
                 "tree": ("reference", "sah")[tr.value] if tr.value >= 0 else None}
 
-    def collect_stats(self, params: N.RenderParams) -> dict:
+    def collect_stats(self, params: N.RenderParams, tree: int = 0) -> dict:
+        """Traversal statistics of one counting-variant render: tree 0 the reference's traversal
+        (hittable.rs:429-473), tree 1 the traversal the product kernel runs (the SAH walk, its
+        leaf-box proofs and re-traced rays, where the world takes it)."""
         s = N.RenderStats()
-        check(lib().rtw_render_collect_stats(self._h, C.byref(params), C.byref(s)))
+        if tree == 0:
+            check(lib().rtw_render_collect_stats(self._h, C.byref(params), C.byref(s)))
+        else:
+            check(lib().rtw_render_collect_stats_tree(self._h, C.byref(params), tree, C.byref(s)))
         return s.as_dict()
 
     DEBUG_COUNTERS = ("trav_calls", "iters", "node_iters", "leaf_iters", "node_lanes", "leaf_lanes",

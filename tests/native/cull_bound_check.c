@@ -1,9 +1,12 @@
 /* Stress test of the proximity cull's error bound (include/rtw_cull.h, rtw_scalar.h rtw_cull_*,
- * DESIGN.md "Proximity cull").  For random spheres and triangles -- grazing/silhouette rays,
- * slivers, near-parallel rays, origins on and far from the surface, scales 1e-2..1e3 -- run the
- * reference's f32 primitive test (sphere_geometry.rs:21-59, triangle_geometry.rs:13-45) with
- * t_range [0.001, te).  Every accepted hit must pass the cull predicate on the leaf's own box
- * (the tightest node that can contain it).  Also reports the largest ratio
+ * DESIGN.md "Proximity cull").  For random spheres, triangles, rects and box primitives, plain and
+ * wrapped in a Y rotation + translation and / or a motion (Transformation / Animation,
+ * hittable.rs:234-244) -- grazing/silhouette rays, slivers, near-parallel rays, origins on and far
+ * from the surface, scales 1e-2..1e3 -- run the reference's f32 primitive test
+ * (sphere_geometry.rs:21-59, triangle_geometry.rs:13-45, rect_geometry.rs:33-59, aabb.rs:80-167)
+ * on the ray the device gives the leaf, with t_range [0.001, te).  Every accepted hit must pass the
+ * cull predicate on the leaf's own cull box (rtw_cull_leaf: the tightest node that can contain it).
+ * Also reports the largest ratio
  *   (distance of the exact point o + t d outside the box) / delta
  * which the bound requires to stay < 1.  Exit status 1 on any violation.
  * Built with -ffp-contract=off like the kernel and the oracle. */
@@ -13,6 +16,10 @@
 #include <stdlib.h>
 
 #include "../../include/rtw_cull.h"
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
 
 static uint64_t s = 0x243F6A8885A308D3ull;
 static inline uint64_t nxt(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
@@ -108,6 +115,48 @@ static V rnd_dir(void) {
     return unit(d);
 }
 
+static int rect_hit(const rtw_rect* g, V o, V d, float ts, float te, float* t) {
+    int p0, p1, n;
+    rtw_rect_axes(g->plane, &p0, &p1, &n);
+    const float tt = (g->dist - o.e[n]) / d.e[n];
+    if (!(ts <= tt && tt < te)) return 0;
+    const V pos = add(o, mul(d, tt));
+    if (!(pos.e[p0] >= g->r0[0] && pos.e[p0] <= g->r0[1] && pos.e[p1] >= g->r1[0] && pos.e[p1] <= g->r1[1])) return 0;
+    *t = tt;
+    return 1;
+}
+
+static int box_hit(const rtw_box* b, V o, V d, float ts, float te, float* t) { /* aabb.rs:80-167 */
+    float near = -INFINITY, far = INFINITY;
+    for (int a = 0; a < 3; ++a) {
+        const float t1 = (b->min[a] - o.e[a]) / d.e[a], t2 = (b->max[a] - o.e[a]) / d.e[a];
+        const float tmin = rtw_minr(t1, t2), tmax = rtw_maxr(t1, t2);
+        if (tmin > near) near = tmin;
+        if (tmax < far) far = tmax;
+        if (near > far || far < 0.0f) return 0;
+    }
+    if (ts <= near && near < te) { *t = near; return 1; }
+    if (ts <= far && far < te) { *t = far; return 1; }
+    return 0;
+}
+
+/* the device's leaf_local_ray: Animation (outermost) then Transformation, xf_reverse each */
+static void local_ray(const rtw_leaf* L, float time, V o, V d, V* lo, V* ld) {
+    if (L->flags & RTW_LEAF_ANIMATION) {
+        const V vt = mul((V){{L->velocity[0], L->velocity[1], L->velocity[2]}}, time);
+        const V off = {{0.0f + vt.e[0], 0.0f + vt.e[1], 0.0f + vt.e[2]}};
+        o = sub(o, off);  /* rot_up(1, -0, .) is exact */
+    }
+    if (L->flags & RTW_LEAF_TRANSFORM) {
+        const float c = L->y_cos, sn = -L->y_sin;
+        const V q = sub(o, (V){{L->offset[0], L->offset[1], L->offset[2]}});
+        o = (V){{c * q.e[0] + sn * q.e[2], q.e[1], -sn * q.e[0] + c * q.e[2]}};
+        d = (V){{c * d.e[0] + sn * d.e[2], d.e[1], -sn * d.e[0] + c * d.e[2]}};
+    }
+    *lo = o;
+    *ld = d;
+}
+
 int main(int argc, char** argv) {
     const long n = argc > 1 ? atol(argv[1]) : 2000000;
     long acc_s = 0, acc_t = 0, bad = 0;
@@ -183,7 +232,114 @@ int main(int argc, char** argv) {
         const double q = outside(lo, hi, o, d, t) / delta_of(lo, hi, k, m, o);
         if (q > worst_t) worst_t = q;
     }
-    printf("sphere hits %ld (max outside/delta %.4f), triangle hits %ld (max outside/delta %.4f), violations %ld\n",
-           acc_s, worst_s, acc_t, worst_t, bad);
-    return bad == 0 && worst_s < 1.0 && worst_t < 1.0 ? 0 : 1;
+    /* rects, boxes and spheres, plain or wrapped (rtw_cull_leaf with wrapped = 1) */
+    long acc_w[3] = {0, 0, 0};
+    double worst_w[3] = {0.0, 0.0, 0.0};
+    const char* wname[3] = {"rect", "box", "wrapped"};
+    for (long it = 0; it < n; ++it) {
+        const double S = LR(1e-2, 1e3);
+        double base[3];
+        for (int i = 0; i < 3; ++i) base[i] = R(-1, 1) * S * LR(1e-3, 1e3);
+        rtw_sphere sp;
+        rtw_rect rc;
+        rtw_box bx;
+        rtw_leaf L = {0};
+        rtw_world w = {0};
+        const int kind = (int)(nxt() % 3);  /* 0 rect, 1 box, 2 sphere */
+        double tgt[3];                      /* a local point on the primitive's surface */
+        if (kind == 0) {
+            rc.plane = (int32_t)(nxt() % 3);
+            int p0, p1, nn;
+            rtw_rect_axes(rc.plane, &p0, &p1, &nn);
+            rc.dist = (float)base[nn];
+            const double a0 = base[p0], a1 = base[p0] + S * LR(1e-3, 1), b0 = base[p1], b1 = base[p1] + S * LR(1e-3, 1);
+            rc.r0[0] = (float)a0; rc.r0[1] = (float)a1; rc.r1[0] = (float)b0; rc.r1[1] = (float)b1;
+            tgt[nn] = rc.dist;
+            const int edge = (int)(nxt() % 3);  /* interior, near the p0 edges, near the p1 edges */
+            tgt[p0] = edge == 1 ? ((nxt() & 1) ? a0 : a1) + R(-1, 1) * LR(1e-9, 1e-4) * S : R(a0, a1);
+            tgt[p1] = edge == 2 ? ((nxt() & 1) ? b0 : b1) + R(-1, 1) * LR(1e-9, 1e-4) * S : R(b0, b1);
+            L.geom_kind = RTW_GEOM_RECT;
+            w.rects = &rc;
+            w.rect_count = 1;
+        } else if (kind == 1) {
+            for (int i = 0; i < 3; ++i) {
+                bx.min[i] = (float)base[i];
+                bx.max[i] = (float)(base[i] + S * LR(1e-3, 1));
+            }
+            const int face = (int)(nxt() % 3);
+            for (int i = 0; i < 3; ++i) tgt[i] = R(bx.min[i], bx.max[i]);
+            tgt[face] = (nxt() & 1) ? bx.min[face] : bx.max[face];
+            if (nxt() & 1) {  /* near an edge */
+                const int e2 = (face + 1 + (int)(nxt() & 1)) % 3;
+                tgt[e2] = ((nxt() & 1) ? bx.min[e2] : bx.max[e2]) + R(-1, 1) * LR(1e-9, 1e-4) * S;
+            }
+            L.geom_kind = RTW_GEOM_BOX;
+            w.boxes = &bx;
+            w.box_count = 1;
+        } else {
+            for (int i = 0; i < 3; ++i) sp.center[i] = (float)base[i];
+            sp.radius = (float)(S * LR(1e-3, 1));
+            const V u = rnd_dir();
+            for (int i = 0; i < 3; ++i) tgt[i] = sp.center[i] + sp.radius * (1.0 + R(-1, 1) * LR(1e-9, 1e-3)) * u.e[i];
+            L.geom_kind = RTW_GEOM_SPHERE;
+            w.spheres = &sp;
+            w.sphere_count = 1;
+        }
+        const int wrapped = kind == 2 || (nxt() & 1);
+        float time = 0.0f;
+        w.camera.time0 = 0.0f;
+        w.camera.time1 = (nxt() & 1) ? 0.0f : (float)LR(1e-2, 4.0);
+        if (wrapped) {
+            const int fl = 1 + (int)(nxt() % 3);  /* transform, animation, both */
+            if (fl & 1) {
+                L.flags |= RTW_LEAF_TRANSFORM;
+                const double ang = R(-M_PI, M_PI);
+                L.y_cos = (float)cos(ang);
+                L.y_sin = (float)sin(ang);
+                for (int i = 0; i < 3; ++i) L.offset[i] = (float)(R(-1, 1) * S * LR(1e-3, 1e3));
+            }
+            if (fl & 2) {
+                L.flags |= RTW_LEAF_ANIMATION;
+                for (int i = 0; i < 3; ++i) L.velocity[i] = (float)(R(-1, 1) * S * LR(1e-3, 10));
+                time = (float)R(w.camera.time0, w.camera.time1);
+            }
+        }
+        /* the target's world position (exact forward map of the local point) */
+        double wt[3] = {tgt[0], tgt[1], tgt[2]};
+        if (L.flags & RTW_LEAF_TRANSFORM) {
+            const double c = L.y_cos, sn = L.y_sin, det = c * c + sn * sn;
+            const double x = wt[0], z = wt[2];
+            wt[0] = (c * x + sn * z) / det + L.offset[0];
+            wt[1] += L.offset[1];
+            wt[2] = (-sn * x + c * z) / det + L.offset[2];
+        }
+        if (L.flags & RTW_LEAF_ANIMATION)
+            for (int i = 0; i < 3; ++i) wt[i] += (double)L.velocity[i] * (double)time;
+        V dd = rnd_dir();
+        const double dist = S * LR(1e-3, 1e4);
+        V o, tv;
+        for (int i = 0; i < 3; ++i) { o.e[i] = (float)(wt[i] + dist * dd.e[i]); tv.e[i] = (float)wt[i]; }
+        const V d = unit(sub(tv, o));
+        const float te = (nxt() & 3) ? INFINITY : (float)(dist * LR(0.5, 2.0));
+        V lo_, ld_;
+        local_ray(&L, time, o, d, &lo_, &ld_);
+        float t;
+        const int hit = kind == 0 ? rect_hit(&rc, lo_, ld_, 0.001f, te, &t)
+                      : kind == 1 ? box_hit(&bx, lo_, ld_, 0.001f, te, &t)
+                                  : sphere_hit((V){{sp.center[0], sp.center[1], sp.center[2]}}, sp.radius, lo_, ld_, 0.001f, te, &t);
+        if (!hit) continue;
+        float k, m, lo[3], hi[3];
+        int never = 0;
+        if (!rtw_cull_leaf(&w, &L, 1, &k, &m, lo, hi, &never) || never) continue;
+        const int cls = wrapped ? 2 : kind;  /* plain spheres are covered above */
+        ++acc_w[cls];
+        if (!cull_pass(lo, hi, k, m, o, d, 0.001f, te)) ++bad;
+        const double q = outside(lo, hi, o, d, t) / delta_of(lo, hi, k, m, o);
+        if (q > worst_w[cls]) worst_w[cls] = q;
+    }
+    printf("sphere hits %ld (max outside/delta %.4f), triangle hits %ld (max outside/delta %.4f)", acc_s, worst_s,
+           acc_t, worst_t);
+    for (int c = 0; c < 3; ++c) printf(", %s hits %ld (max outside/delta %.4f)", wname[c], acc_w[c], worst_w[c]);
+    printf(", violations %ld\n", bad);
+    return bad == 0 && worst_s < 1.0 && worst_t < 1.0 && worst_w[0] < 1.0 && worst_w[1] < 1.0 && worst_w[2] < 1.0 ? 0 : 1;
 }

@@ -147,7 +147,8 @@ def _kernel_tree(world) -> str:
     return dw.kernel_variant()["tree"]
 
 
-@pytest.mark.parametrize("name", ["final_scene1", "suzanne"])
+@pytest.mark.parametrize("name", ["final_scene1", "suzanne", "cornell_cube", "cornell_box", "earth_motion",
+                                  "moving_spheres", "defocus_blur", "simple_plane"])
 def test_sah_tree_agrees(worlds, name, monkeypatch):
     """closest hits found on the kernel's SAH tree (verified against the reference
     tree's order, re-traced there where the proof fails) give the reference-tree loop's bits
@@ -189,6 +190,41 @@ def _tie_world():
     g.add(wb.new_mesh(quad, mats[2]))
     cam = R.Camera.build().vertical_fov(40.0, 9.0 / 16.0).position((0.3, 1.2, 5.0)).look_at((0, 1, 0), (0, 0.5, 0)).build()
     return g.build().finish(wb, R.BackgroundColor.sky(), cam)
+
+
+def _tie_world_wrapped():
+    """Ties among rects, boxes and wrapped leaves: two coincident rects of different materials, a
+    rotated box twice over (its reference Aabb is the untransformed box, the apply_aabb quirk, so
+    many of its hits lie outside that box: the proof falls back to the reference tree there), a box
+    face flush with a rect, and two coincident moving spheres under motion blur."""
+    wb = R.WorldBuilder()
+    mats = [wb.material_lambert_solid((0.8, 0.2, 0.2)), wb.material_lambert_solid((0.2, 0.8, 0.2)),
+            wb.material_metal_solid((0.7, 0.7, 0.7), 0.1), wb.material_dielectric(1.5)]
+    g = wb.new_group()
+    g.add(wb.new_obj_sphere(100.0, mats[0]).translate((0.0, -100.0, 0.0)))
+    g.add(wb.new_obj_rect_xy((0.0, 1.0, -1.0), 4.0, 2.0, mats[0]))
+    g.add(wb.new_obj_rect_xy((0.0, 1.0, -1.0), 4.0, 2.0, mats[1]))
+    for m in (mats[1], mats[2]):
+        g.add(wb.new_obj_box(0.8, 0.8, 0.8, m).rotate_around_up(25.0).translate((-1.0, 0.4, 0.3)))
+    g.add(wb.new_obj_box(0.6, 0.6, 0.6, mats[3]).translate((1.2, 0.3, -0.7)))
+    g.add(wb.new_obj_rect_yz((1.5, 0.3, -0.7), 0.6, 0.6, mats[1]))
+    for m in (mats[0], mats[3]):
+        g.add(wb.new_obj_sphere(0.3, m).translate((0.6, 1.4, 0.5)).animate_moving((0.0, 0.5, 0.0)))
+    cam = (R.Camera.build().vertical_fov(40.0, 9.0 / 16.0).position((0.3, 1.2, 5.0)).look_at((0, 1, 0), (0, 0.5, 0))
+           .motion_blur(0.0, 1.0).build())
+    return g.build().finish(wb, R.BackgroundColor.sky(), cam)
+
+
+def test_sah_wrapped_ties_and_grazing_hits(monkeypatch):
+    world = _tie_world_wrapped()
+    assert _kernel_tree(world) == "sah"
+    size = R.Size2i(96, 54)
+    gpu = R.render(size, 1, 8, 50, world, seed=37)
+    assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=37)), "wrapped tie world")
+    big = R.Size2i(480, 270)
+    sah = R.render(big, 1, 4, 50, world, seed=37)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert_bit_identical(sah, R.render(big, 1, 4, 50, world, seed=37), "wrapped tie world, SAH vs reference tree")
 
 
 def test_sah_ties_and_grazing_hits(monkeypatch):

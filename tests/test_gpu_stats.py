@@ -55,3 +55,27 @@ def test_cull_invariance_large(worlds, name, size, spp, monkeypatch):
     """Size-independent property at a large sample count: culled == reference traversal, bitwise."""
     culled, plain = _render_pair(worlds(name), size, spp, 77, monkeypatch)
     assert_bit_identical(culled, plain, name)
+
+
+@pytest.mark.parametrize("name", ["final_scene1", "suzanne", "cornell_cube"])
+def test_kernel_tree_counts(worlds, name):
+    """Counting variant of the traversal the product kernel runs (rtw_render_collect_stats_tree 1,
+    the input of bench.py's record bytes): the same paths as the reference's traversal -- samples,
+    rays, closest hits per primitive kind, material and texel reads equal -- with the SAH walk's own
+    node and leaf visits, fewer than the reference tree's on the SAH worlds."""
+    import torch
+
+    world = worlds(name)
+    p = R.render_params(R.Size2i(48, 32), 4, 50, seed=5)
+    dw = R.DeviceWorld(world, 0)
+    out = torch.zeros(48 * 32 * 3, dtype=torch.float32, device="cuda:0")
+    dw.render_into(p, out.data_ptr(), torch.cuda.current_stream().cuda_stream)  # sets kernel_variant()
+    torch.cuda.synchronize()
+    ref = dw.collect_stats(p, tree=0)
+    own = dw.collect_stats(p, tree=1)
+    same = ["samples", "rays", "sphere_hits", "rect_hits", "box_hits", "triangle_hits", "material_reads", "texel_reads"]
+    assert {k: own[k] for k in same} == {k: ref[k] for k in same}
+    if dw.kernel_variant()["tree"] == "sah":
+        assert own["node_visits"] < ref["node_visits"]
+    else:
+        assert own == ref

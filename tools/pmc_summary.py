@@ -1,4 +1,4 @@
-"""Summarise tools/prof_pmc.sh output: render-kernel counters and derived ratios.
+"""Summarise tools/gpu_pmc3.sh output: render-kernel counters and derived ratios.
 
 python tools/pmc_summary.py gpurun_out/pmc [stats.json]
 """
