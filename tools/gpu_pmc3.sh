@@ -1,10 +1,10 @@
 # PMC passes (one counter group per rocprofv3 run) of the render kernel on one scene:
-#   SCENE=final_scene1 SPP=32 bash tools/gpu_pmc3.sh  -> gpurun_out/pmc3_<scene>/summary.txt
+#   SCENE=final_scene1 [W=1920 H=1080] SPP=32 bash tools/gpu_pmc3.sh  -> gpurun_out/pmc3_<scene>/summary.txt
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 SC=${SCENE:-final_scene1}
 D=gpurun_out/pmc3_$SC; mkdir -p $D
-P="python3 tools/prof_render.py --scene $SC --spp ${SPP:-32} --repeat 2"
+P="python3 tools/prof_render.py --scene $SC --width ${W:-1920} --height ${H:-1080} --spp ${SPP:-32} --repeat 2"
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/kt -o kt --output-format csv -- $P > $D/kt.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_WAVE_CYCLES -d $D/p1 -o p1 --output-format csv -- $P > $D/p1.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH -d $D/p2 -o p2 --output-format csv -- $P > $D/p2.log 2>&1 || exit $?
