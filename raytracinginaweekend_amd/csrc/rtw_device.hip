@@ -197,6 +197,10 @@ struct KArgs {
     TuneState* tune;          // in-frame threshold tuning, or null
     int32_t mk_world;         // node coordinates admit the per-ray exact-division guard (ray_pre)
     int32_t stats_tree;       // counting variant: 0 the reference tree, 1 the tree the product kernel walks
+    // shading tables in LDS (float4 offsets, -1: read from HBM / L2): leaf records, materials and, in
+    // solid-texture worlds, each texture's first record; the stack follows them (stack_off)
+    int32_t sh_li, sh_mat, sh_tex0, stack_off;
+    int32_t material_count, texture_count;
     int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
                               // re-traced on the reference tree where the proof does not hold (§5.6)
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
@@ -549,8 +553,18 @@ __device__ __forceinline__ void from_ray(Hit& h, const Ray& r, V3 pos, V3 sn, fl
     h.u = u;
     h.v = v;
 }
-__device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray& r, float t, Hit& h) {
-    const int4 info = w.leaf_info[leaf];
+// Where shading reads its per-leaf, material and texture records: LDS float4 offsets (-1: HBM / L2).
+// The chain leaf record -> material -> texture is a run of dependent loads per shaded ray, so the
+// tables sit in LDS whenever they fit (launch_render), and a plain sphere's geometry comes from
+// its leaf_fast copy (`fast`, also in LDS).
+extern __shared__ __attribute__((aligned(16))) float4 smem[];
+struct ShadeTabs {
+    int32_t li, mat, tex0, fast;
+};
+__device__ __forceinline__ int4 lds_i4(int32_t i) { return reinterpret_cast<const int4*>(smem)[i]; }
+__device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray& r, float t, Hit& h,
+                                            const ShadeTabs& S) {
+    const int4 info = S.li >= 0 ? lds_i4(S.li + leaf) : w.leaf_info[leaf];
     const uint32_t flags = (uint32_t)info.w;
     const Ray rr = leaf_local_ray(w, leaf, flags, r);
     const int kind = info.x, idx = info.y;
@@ -561,7 +575,9 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         h.v = 0.0f;
         h.front = false;
     } else if (kind == RTW_GEOM_SPHERE) {  // sphere_geometry.rs:42-52
-        const float4 s = w.spheres[idx];
+        // a plain sphere's leaf_fast record is {centre, radius} (the same floats as spheres[idx])
+        const float4 s = (S.fast >= 0 && (flags & (RTW_LEAF_TRANSFORM | RTW_LEAF_ANIMATION)) == 0)
+                             ? smem[S.fast + leaf] : w.spheres[idx];
         const V3 pos = at(rr, t);
         const V3 sn = divs(sub(pos, v3(s.x, s.y, s.z)), s.w);
         // uv (vec3.rs:241-249) only reaches the image through an image texture; a pure function
@@ -874,9 +890,10 @@ __device__ __forceinline__ float marble_k(const float* ranvec, const uint32_t* p
 // TX: the world's textures are all SolidColor (TX_SOLID) or not (TX_ANY: checker, marble, image)
 enum { TX_SOLID = 0, TX_ANY = 1 };
 template <bool STATS, int TX>
-__device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit& h, Stats& st) {  // texture.rs:23-53
+__device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit& h, Stats& st,
+                                             const ShadeTabs& S) {  // texture.rs:23-53
     for (int guard = 0; guard < 64; ++guard) {
-        const int4 t0 = w.textures[3 * tex];
+        const int4 t0 = S.tex0 >= 0 ? lds_i4(S.tex0 + tex) : w.textures[3 * tex];
         const int kind = t0.x;
         if (TX == TX_SOLID || kind == RTW_TEX_SOLID)
             return v3(__int_as_float(t0.y), __int_as_float(t0.z), __int_as_float(t0.w));
@@ -987,7 +1004,7 @@ struct ShadeOut {
 
 template <bool STATS, int TX>
 __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t mode, Path P, int32_t found, float te,
-                                       float pdot) {
+                                       float pdot, const ShadeTabs& S) {
     const DWorld& w = *wp;
     Stats st;
     st.c[ST_TEXEL] = 0;
@@ -1000,7 +1017,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
     bool done = false;
     if (found >= 0) {
         Hit h;
-        leaf_record(w, found, ray, te, h);
+        leaf_record(w, found, ray, te, h, S);
         if (mode == RTW_MODE_NORMALS) {  // rendering.rs:110-113
             color = mul(add(h.n, v3(1.0f, 1.0f, 1.0f)), 0.5f);
             done = true;
@@ -1008,7 +1025,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
             color = v3(0.0f, 0.0f, 0.0f);
             done = true;
         } else {
-                const int4 M = w.materials[h.material];
+                const int4 M = S.mat >= 0 ? lds_i4(S.mat + h.material) : w.materials[h.material];
                 const int mkind = M.x;
                 // Material::scatter (material.rs:52-114).  At most one texture lookup per bounce:
                 // the albedo of a scattering material or the emission of a DiffuseLight.
@@ -1077,7 +1094,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                         sdir = sv;
                     }
                 }
-                const V3 tc = (tex >= 0) ? texture_sample<STATS, TX>(w, tex, h, st) : v3(0.0f, 0.0f, 0.0f);
+                const V3 tc = (tex >= 0) ? texture_sample<STATS, TX>(w, tex, h, st, S) : v3(0.0f, 0.0f, 0.0f);
                 const V3 emitted = (mkind == RTW_MAT_DIFFUSE_LIGHT) ? tc : v3(0.0f, 0.0f, 0.0f);
                 const V3 albedo = (mkind == RTW_MAT_DIELECTRIC) ? v3(1.0f, 1.0f, 1.0f) : tc;
                 if (scatters) {
@@ -1139,8 +1156,6 @@ __device__ unsigned long long rtw_phase_cycles[8];
 #define RTW_PT(k) do { } while (0)
 #define RTW_PT_FLUSH do { } while (0)
 #endif
-
-extern __shared__ __attribute__((aligned(16))) float4 smem[];
 
 // Traversal state of one lane (by value, in registers, across the out-of-line call).
 struct Trav {
@@ -1404,12 +1419,21 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             float4* tris = rects + 2 * A.rect_count;
             for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[i] = w.tri_fast[i];
         }
+        if (A.sh_li >= 0) {  // shading tables (launch_render decides whether they fit)
+            int4* li = reinterpret_cast<int4*>(smem + A.sh_li);
+            for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) li[i] = w.leaf_info[i];
+            int4* mt = reinterpret_cast<int4*>(smem + A.sh_mat);
+            for (int i = threadIdx.x; i < A.material_count; i += RTW_BLOCK) mt[i] = w.materials[i];
+            if (A.sh_tex0 >= 0) {
+                int4* tx = reinterpret_cast<int4*>(smem + A.sh_tex0);
+                for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
+            }
+        }
         __syncthreads();
     }
-    // the traversal stacks follow the LDS scene
-    const int32_t stack_off =
-        LDS_SCENE ? 2 * A.node_count + A.leaf_count + (A.node_count + 1) / 2 + 2 * A.rect_count + (LDS == 2 ? 4 * A.tri_count : 0)
-                  : 0;
+    // the traversal stacks follow the LDS scene and the shading tables
+    const int32_t stack_off = LDS_SCENE ? A.stack_off : 0;
+    const ShadeTabs stabs{A.sh_li, A.sh_mat, A.sh_tex0, A.sh_li >= 0 ? 2 * A.node_count : -1};
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
@@ -1733,7 +1757,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             P.acc = acc;
             P.depth = depth;
             P.rng = T.rng;
-            const ShadeOut so = shade<STATS, TX>(A.wdev, A.mode, P, T.found, T.te, pdot);
+            const ShadeOut so = shade<STATS, TX>(A.wdev, A.mode, P, T.found, T.te, pdot, stabs);
             T.ray = so.p.ray;
             att = so.p.att;
             acc = so.p.acc;
@@ -2217,7 +2241,7 @@ struct rtw_gpu_world {
     DWorld w{};
     const DWorld* wdev = nullptr;
     int32_t node_count = 0, leaf_count = 0, depth = 1;
-    int32_t tri_count = 0, rect_count = 0;
+    int32_t tri_count = 0, rect_count = 0, material_count = 0, texture_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int32_t sah_nodes = 0;  // nodes of the SAH tree, 0: the world takes the reference tree only (§5.6)
     int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
@@ -2488,6 +2512,8 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     }
     g->tri_count = w->triangle_count;
     g->rect_count = w->rect_count;
+    g->material_count = w->material_count;
+    g->texture_count = w->texture_count;
     g->mk_world = 1;
     g->leaf_kinds = LK_SPHERES;
     g->tex_kinds = TX_SOLID;
@@ -2604,6 +2630,9 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.mk_world = g->mk_world;
     A.tri_count = g->tri_count;
     A.rect_count = g->rect_count;
+    A.material_count = g->material_count;
+    A.texture_count = g->texture_count;
+    A.sh_li = A.sh_mat = A.sh_tex0 = -1;
     A.queue = g->queue;
     A.wdev = g->wdev;
     A.trace_min = 32;
@@ -2647,7 +2676,17 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         mode = 2;
     else if (scene_bytes + stack_bytes <= cap) mode = 1;
     if (const char* e = std::getenv("RTW_LDS_MODE")) mode = std::min(mode, std::atoi(e));  // audits: cap the mode
-    const size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes + stack16_bytes : stack_bytes);
+    size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes + stack16_bytes : stack_bytes);
+    // shading tables after the scene when they fit too (RTW_NO_SHADE_LDS=1: keep them in HBM / L2)
+    const int32_t scene_f4 = (int32_t)((scene_bytes + (mode == 2 ? tri_bytes : 0)) / sizeof(float4));
+    const size_t sh_bytes = (size_t)(g->leaf_count + A.material_count + (tx == TX_SOLID ? A.texture_count : 0)) * sizeof(int4);
+    const char* nsl = std::getenv("RTW_NO_SHADE_LDS");
+    const bool sh = mode >= 1 && lds + sh_bytes <= cap && !(nsl && nsl[0] && nsl[0] != '0');
+    A.sh_li = sh ? scene_f4 : -1;
+    A.sh_mat = sh ? scene_f4 + g->leaf_count : -1;
+    A.sh_tex0 = sh && tx == TX_SOLID ? scene_f4 + g->leaf_count + A.material_count : -1;
+    A.stack_off = scene_f4 + (sh ? (int32_t)(sh_bytes / sizeof(int4)) : 0);
+    if (sh) lds += sh_bytes;
     using KFn = void (*)(KArgs);
 #define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}
     static const KFn fns[2][5][3] = {
