@@ -74,6 +74,8 @@
 #endif
 #define RTW_STACK 32    // per-lane traversal stack (LDS), >= the BVH depth (checked at upload)
 #ifndef RTW_LDS_SCENE_MAX
+#define RTW_COOP_MAX 4       // drain: live lanes at most for the wave-cooperative trace (RTW_COOP_MAX=0: off)
+#define RTW_COOP_LEAVES 4096 // ... in worlds of at most this many leaves
 #define RTW_LDS_SCENE_MAX (160 * 1024)  // LDS bytes per block the scene (+ stack) may take
 #endif
 
@@ -203,6 +205,8 @@ struct KArgs {
     int32_t material_count, texture_count;
     int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
                               // re-traced on the reference tree where the proof does not hold (§5.6)
+    int32_t coop_max;         // drain: a wave with at most this many live lanes traces each ray with all
+                              // 64 lanes over every leaf (coop_trace); 0: never
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
     // work order by measured cost (render_frame): costlier tiles first, all their samples together
     const uint32_t* tile_perm;  // tile rank -> local tile, null: chunk-major order
@@ -1132,10 +1136,15 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
 #ifdef RTW_WAVE_TIMING  // experiment builds: per-wave start / end / queue-empty wall clocks of the last launch
 __device__ unsigned long long rtw_wave_times[3 * 8192];
 __device__ unsigned long long rtw_wave_dry[8192];  // first time a lane of the wave found the queue empty
+// per wave after the queue ran dry: busy lanes then, samples finished, their bounces (sum, max),
+// cooperative rays, reference-tree re-traces, wall ticks in the re-traces and in the SAH walk + coop
+__device__ unsigned long long rtw_wave_extra[8 * 8192];
 #endif
 
 // PH_REF: the ray is traced on the reference tree (the SAH path's fallback, §5.6)
-enum { PH_PIXEL = 0, PH_TRACE = 1, PH_SHADE = 2, PH_REF = 3 };
+// PH_DONE: the queues are empty and the lane's last path is finished (it stays in the loop, masked
+// by its phase, so that the wave's remaining rays can be traced with all 64 lanes: coop_trace)
+enum { PH_PIXEL = 0, PH_TRACE = 1, PH_SHADE = 2, PH_REF = 3, PH_DONE = 4 };
 // traversal modes: the reference tree (DFS of hittable.rs:429-473 with hit_cond AND the cull), the
 // SAH tree (cull only, closest hit with ties flagged), the reference tree for PH_REF lanes with
 // the scene in HBM (the LDS holds the SAH tree)
@@ -1191,7 +1200,7 @@ enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_WRAPPED = 3, LK_ANY = 4 };
 template <bool STATS, int LDS, int LK, bool FAST_ONLY, int TM = TM_REF>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
                                       int32_t n_leaves, int32_t n_rects, int32_t n_tris, int32_t stack_off,
-                                      unsigned long long* dbg) {
+                                      unsigned long long* dbg, int32_t coop_exit = -1) {
     // the LDS holds the tree this mode walks (the SAH tree in SAH mode); the fallback reads HBM
     constexpr bool LDS_SCENE = LDS >= 1 && TM != TM_FALLBACK;
     constexpr int ACT = TM == TM_FALLBACK ? PH_REF : PH_TRACE;  // the lanes this loop advances
@@ -1260,9 +1269,11 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         // (rare lanes) runs to the end
         if (TM != TM_FALLBACK && (uint32_t)__popcll(tr) < (uint32_t)trace_min && __ballot(T.phase == PH_SHADE) != 0)
             break;
+        // the drain: the last few tracing lanes (the long walks) go to coop_trace
+        if (TM == TM_SAH && (int32_t)__popcll(tr) <= coop_exit) break;
         if (STATS) {
             const unsigned long long lm = __ballot(T.phase == ACT && T.node < 0);
-            const uint32_t alive = (uint32_t)__popcll(__ballot(1));
+            const uint32_t alive = (uint32_t)__popcll(__ballot(T.phase != PH_DONE));
             const uint32_t waiting = (uint32_t)__popcll(__ballot(T.phase == PH_SHADE));
             if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
                 db[DB_ITERS]++;
@@ -1392,6 +1403,77 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     return T;
 }
 
+// The frame's drain (§5.7): once the queues are empty a wave's last paths run alone, and a path
+// trapped inside suzanne's mesh walks nearly every node and triangle on each of its ~50 bounces
+// (~15 ms on one lane, the 8-GPU shares' tail).  When at most coop_max lanes are still live, each
+// SAH ray of the wave is traced by all 64 lanes instead: lane i tests leaves i, i+64, ... with the
+// walk's own leaf tests at te = inf, and a wave reduction takes the smallest root.  That is the
+// walk's answer (§5.5 step 1: the walk keeps the smallest root over all leaves, and a leaf's first
+// root in [ts, te) is its first root in [ts, inf) whenever that lies below te), and a second leaf
+// with exactly that root sets the tie flag as the walk's take() does.  Plain spheres, rects and
+// triangles only (LK <= LK_PLAIN).  The lane's ray leaves in PH_SHADE with te = succ(t), ready for
+// the proof step that follows the walk.
+template <int LDS, int LK>
+__device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, int32_t n_nodes, int32_t n_leaves,
+                                        int32_t n_rects) {
+    const DWorld& w = *wp;
+    constexpr bool LDS_SCENE = LDS >= 1;
+    const int32_t rect_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
+    const int32_t tri_off = rect_off + 2 * n_rects;
+    const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
+    const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
+    const float4* fast = LDS_SCENE ? smem + 2 * n_nodes : uniform_ptr(w.leaf_fast);
+    const int lane = threadIdx.x & 63;
+    unsigned long long todo = __ballot(T.phase == PH_TRACE && (T.fast & RTW_TF_SAH) != 0);
+    while (todo) {  // wave-uniform: one ray at a time
+        const int src = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        Ray r;
+        r.o = v3(__shfl(T.ray.o.x, src), __shfl(T.ray.o.y, src), __shfl(T.ray.o.z, src));
+        r.d = v3(__shfl(T.ray.d.x, src), __shfl(T.ray.d.y, src), __shfl(T.ray.d.z, src));
+        r.time = __shfl(T.ray.time, src);
+        float best = F32_INF;
+        int32_t bl = -1;
+        uint32_t cnt = 0;  // leaves of this lane reporting exactly `best`
+        for (int32_t leaf = lane; leaf < n_leaves; leaf += 64) {
+            const float4 sph = fast[leaf];
+            float t;
+            bool hit;
+            if (LK == LK_SPHERES || sph.w == sph.w) {
+                hit = sphere_t(sph, r, 0.001f, F32_INF, t);
+            } else if (LK >= LK_PLAIN && __float_as_int(sph.x) == 2) {
+                const int ri = __float_as_int(sph.y);
+                const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
+                const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
+                V3 pos;
+                hit = rect_t(g, r, 0.001f, F32_INF, t, pos);
+            } else {
+                hit = tri_test(load_tri(tri_fast, __float_as_int(sph.y)), r, 0.001f, F32_INF, t);
+            }
+            if (hit) {
+                cnt = t == best ? cnt + 1 : t < best ? 1u : cnt;
+                bl = t < best ? leaf : bl;
+                best = t < best ? t : best;
+            }
+        }
+        float m = best;
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) m = rtw_minr(m, __shfl_xor(m, k));
+        const unsigned long long at = __ballot(bl >= 0 && best == m);
+        const bool tie = __popcll(at) >= 2 || __ballot(bl >= 0 && best == m && cnt >= 2) != 0;
+        const int win = at ? __ffsll((long long)at) - 1 : 0;
+        const int32_t found = at ? __shfl(bl, win) : -1;
+        if (lane == src) {
+            T.found = found;
+            T.te = found >= 0 ? __int_as_float(__float_as_int(m) + 1) : F32_INF;  // succ(t), as take()
+            T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
+            T.sp = 0;
+            T.phase = PH_SHADE;
+        }
+    }
+    return T;
+}
+
 template <bool STATS, int LDS, int LK, int TX>
 __device__ __forceinline__ void render_body(const KArgs& A) {
     constexpr bool LDS_SCENE = LDS >= 1;
@@ -1501,10 +1583,15 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         pf_lane = leader;
     };
     RTW_PT_DECL
+#ifdef RTW_WAVE_TIMING
+    uint32_t wx_busy = 0, wx_n = 0, wx_sum = 0, wx_max = 0, wx_coop = 0, wx_ref = 0;
+    uint64_t wx_tref = 0, wx_tsah = 0, wx_tcoop = 0;
+    bool wx_dry = false;
+#endif
     for (;;) {
+        if (__ballot(T.phase != PH_DONE) == 0) break;  // wave-uniform: every lane is done
         // 1. lanes without a pixel take the next items of the wave's reserve
         RTW_PT(1);
-        bool out_of_work = false;
         for (;;) {
             const unsigned long long m = __ballot(T.phase == PH_PIXEL);
             if (m == 0) break;
@@ -1515,10 +1602,11 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     if (wv_ < 8192) atomicMin(&rtw_wave_dry[wv_], (unsigned long long)wall_clock64());
                 }
 #endif
-                if (T.phase == PH_PIXEL) {
-                    out_of_work = true;
-                    T.phase = PH_TRACE;  // leaves the loops below
-                }
+#ifdef RTW_WAVE_TIMING
+                if (!wx_dry) wx_busy = (uint32_t)__popcll(__ballot(T.phase != PH_PIXEL));
+                wx_dry = true;
+#endif
+                if (T.phase == PH_PIXEL) T.phase = PH_DONE;
                 continue;
             }
             const int leader = __ffsll((long long)m) - 1;
@@ -1636,7 +1724,6 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 qfail = 0;
             }
         }
-        if (out_of_work) break;
 
         // 2. a new ray starts at the root (Scene::hit with t_range 0.001..inf, rendering.rs:25)
         RTW_PT(2);
@@ -1671,9 +1758,30 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         // (almost) every ray is Markstein-exact: such calls run a loop without the true-division
         // path (wave-uniform choice per call)
         if (sah) {
+            // the drain: the walk stops when at most coop_max lanes still trace, and those rays (the
+            // long walks) are traced by the whole wave (coop_trace); wave-uniform condition
+            const bool dry_coop = !STATS && LK <= LK_PLAIN && qfail >= RTW_QUEUES && A.coop_max > 0;
+#ifdef RTW_WAVE_TIMING
+            uint64_t wx_t0 = wall_clock64();
+#endif
             T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
                                                        A.leaf_count, A.rect_count, A.tri_count, stack_off,
-                                                       STATS ? A.stats + ST_COUNT : nullptr);
+                                                       STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
+            if (dry_coop) {
+                const unsigned long long tm = __ballot(T.phase == PH_TRACE);
+#ifdef RTW_WAVE_TIMING
+                if (tm != 0 && (uint32_t)__popcll(tm) <= (uint32_t)A.coop_max) wx_coop += (uint32_t)__popcll(tm);
+                const uint64_t wx_tc = wall_clock64();
+                wx_tsah += wx_tc - wx_t0;  // the walk part
+                wx_t0 = wx_tc;
+#endif
+                if (tm != 0 && (uint32_t)__popcll(tm) <= (uint32_t)A.coop_max)
+                    T = coop_trace<LDS, LK>(A.wdev, T, A.node_count, A.leaf_count, A.rect_count);
+            }
+#ifdef RTW_WAVE_TIMING
+            const uint64_t wx_t1 = wall_clock64();
+            if (qfail >= RTW_QUEUES) wx_tcoop += wx_t1 - wx_t0;
+#endif
             if (STATS) {
                 st.c[ST_NODES] += T.n_nodes;
                 st.c[ST_T_SPHERE] += T.n_sph_rect & 0xFFFFu;
@@ -1711,10 +1819,17 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     T.found = -1;
                 }
             }
+#ifdef RTW_WAVE_TIMING
+            if (qfail >= RTW_QUEUES) wx_ref += (uint32_t)__popcll(__ballot(T.phase == PH_REF));
+            const uint64_t wx_t2 = wall_clock64();
+#endif
             if (__ballot(T.phase == PH_REF) != 0)
                 T = traverse<STATS, LDS, LK, false, TM_FALLBACK>(A.wdev, T, 0, A.node_count, A.leaf_count, A.rect_count,
                                                                  A.tri_count, stack_off,
                                                                  STATS ? A.stats + ST_COUNT : nullptr);
+#ifdef RTW_WAVE_TIMING
+            if (qfail >= RTW_QUEUES) wx_tref += wall_clock64() - wx_t2;
+#endif
         } else if (__ballot(T.phase == PH_TRACE && (T.fast & 8) == 0) == 0) {
             T = traverse<STATS, LDS, LK, true>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
                                                A.leaf_count, A.rect_count, A.tri_count, stack_off,
@@ -1775,6 +1890,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 // slot for the next frame's work order
                 const int32_t bounces = A.max_depth - depth;
                 if (!STATS && A.slot_cost && bounces > 3) atomicAdd(&A.slot_cost[slot], (uint32_t)bounces);
+#ifdef RTW_WAVE_TIMING
+                if (qfail >= RTW_QUEUES) {
+                    ++wx_n;
+                    wx_sum += (uint32_t)bounces;
+                    wx_max = max(wx_max, (uint32_t)bounces);
+                }
+#endif
                 ++sample;
                 if (sample >= sample_end) T.phase = PH_PIXEL;
                 else start_sample();
@@ -1784,6 +1906,25 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         }
     }
     RTW_PT_FLUSH;
+#ifdef RTW_WAVE_TIMING
+    {
+        const uint32_t wv_ = (blockIdx.x * RTW_BLOCK + threadIdx.x) / 64;
+        if (wv_ < 8192) {
+            unsigned long long* x = rtw_wave_extra + 8 * wv_;
+            if (wx_busy) atomicMax(&x[0], (unsigned long long)wx_busy);
+            atomicAdd(&x[1], (unsigned long long)wx_n);
+            atomicAdd(&x[2], (unsigned long long)wx_sum);
+            (void)wx_max;
+            if (lane == 0) {  // wave-level sums (identical in every lane)
+                x[4] = wx_coop;
+                x[5] = wx_ref;
+                x[6] = wx_tref;
+                x[7] = wx_tsah;
+                x[3] = wx_tcoop;  // (replaces max bounces)
+            }
+        }
+    }
+#endif
     if (STATS) {
         for (int i = 0; i < ST_COUNT; ++i)
             if (st.c[i]) atomicAdd(&A.stats[i], (unsigned long long)st.c[i]);
@@ -2276,6 +2417,20 @@ extern "C" RTW_API int rtw_debug_wave_times(unsigned long long* out24576) {
     return rtw::fail(RTW_ERR_UNSUPPORTED, "built without RTW_WAVE_TIMING");
 #endif
 }
+// experiment builds: per-wave drain counters of the launches since the last call (busy lanes when
+// the queue ran dry: max; samples finished after it, their bounces: sums; max bounces), then reset
+extern "C" RTW_API int rtw_debug_wave_extra(unsigned long long* out65536) {
+#ifdef RTW_WAVE_TIMING
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out65536, HIP_SYMBOL(rtw_wave_extra), 8 * 8192 * sizeof(unsigned long long)));
+    std::vector<unsigned long long> z(8 * 8192, 0);
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rtw_wave_extra), z.data(), z.size() * sizeof(unsigned long long)));
+    return RTW_OK;
+#else
+    (void)out65536;
+    return rtw::fail(RTW_ERR_UNSUPPORTED, "built without RTW_WAVE_TIMING");
+#endif
+}
 
 // experiment builds (-DRTW_PHASE_TIMING): read and reset the phase cycle sums
 extern "C" RTW_API int rtw_debug_phase_cycles(unsigned long long* out8) {
@@ -2649,6 +2804,7 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
 // Launch the persistent render kernel: zero the pixel queue, stage the scene in LDS when it
 // fits, size the grid to the resident block count.
 enum LaunchKind { LK_RENDER, LK_STATS };
+size_t env_size(const char* name, size_t dflt);
 int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const bool stats = kind == LK_STATS;
     const bool ktree = stats && A.stats_tree == 1;  // count the product kernel's own traversal
@@ -2660,6 +2816,10 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     // the SAH tree (§5.6) replaces the reference tree in LDS; the counting variant keeps the latter
     const bool sah = (!stats || ktree) && g->sah_nodes > 0 && g->mk_world && lk <= LK_WRAPPED;
     A.sah = sah ? 1 : 0;
+    // the drain's cooperative trace (coop_trace): worlds small enough to test every leaf per ray
+    A.coop_max = g->leaf_count <= RTW_COOP_LEAVES ? (int32_t)env_size("RTW_COOP_MAX", RTW_COOP_MAX) : 0;
+    if (const char* e = std::getenv("RTW_COOP_MAX"))
+        if (e[0] == '0') A.coop_max = 0;
     A.node_count = sah ? g->sah_nodes : g->node_count;
     const size_t scene_bytes =
         (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
