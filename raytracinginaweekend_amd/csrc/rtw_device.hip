@@ -111,6 +111,10 @@ struct DWorld {
     const float4* sah_b;
     const float2* sah_km;
     const float4* leaf_box;
+    // each leaf's place in the reference tree's DFS (coop_trace's tie resolution): {side bits, and
+    // per axis the bits of the ancestors splitting on it}, bit 31 - k for the ancestor at depth k;
+    // null when the reference tree is deeper than 32
+    const uint4* leaf_key;
     int32_t sah_root;
     int32_t root;
     int32_t has_light;
@@ -207,6 +211,7 @@ struct KArgs {
                               // re-traced on the reference tree where the proof does not hold (§5.6)
     int32_t coop_max;         // drain: a wave with at most this many live lanes traces each ray with all
                               // 64 lanes over every leaf (coop_trace); 0: never
+    int32_t coop_ties;        // 1: the walk's tied rays are resolved by coop_trace (else re-traced); 2: audit
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
     // work order by measured cost (render_frame): costlier tiles first, all their samples together
     const uint32_t* tile_perm;  // tile rank -> local tile, null: chunk-major order
@@ -1410,12 +1415,18 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 // walk's own leaf tests at te = inf, and a wave reduction takes the smallest root.  That is the
 // walk's answer (§5.5 step 1: the walk keeps the smallest root over all leaves, and a leaf's first
 // root in [ts, te) is its first root in [ts, inf) whenever that lies below te), and a second leaf
-// with exactly that root sets the tie flag as the walk's take() does.  Plain spheres, rects and
-// triangles only (LK <= LK_PLAIN).  The lane's ray leaves in PH_SHADE with te = succ(t), ready for
-// the proof step that follows the walk.
+// with exactly that root makes a tie.  Plain spheres, rects and triangles only (LK <= LK_PLAIN).
+// The lane's ray leaves in PH_SHADE with te = succ(t), ready for the proof step that follows the walk.
+// Ties are resolved here: the reference takes the tied leaf its DFS visits first (hittable.rs:453-460:
+// te narrows to t, and an equal root is not inside the narrowed range), and it does visit that leaf
+// when the leaf's proof box passes at succ(t) -- before it, te > t as no smaller root exists.  So the
+// tied leaf first in DFS order (leaf_key) is returned without the tie flag, and the proof step
+// decides as for any hit; a lane holding two tied leaves keeps the flag (re-traced on the reference
+// tree).  Rays of `todo` only (SAH rays: RTW_TF_SAH).  `audit` (tests only, RTW_COOP_AUDIT=1) takes
+// the DFS-last tied leaf instead: wrong images, which shows that the resolution decides them.
 template <int LDS, int LK>
-__device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, int32_t n_nodes, int32_t n_leaves,
-                                        int32_t n_rects) {
+__device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, unsigned long long todo, int32_t n_nodes,
+                                        int32_t n_leaves, int32_t n_rects, bool audit) {
     const DWorld& w = *wp;
     constexpr bool LDS_SCENE = LDS >= 1;
     const int32_t rect_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
@@ -1424,7 +1435,7 @@ __device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, i
     const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
     const float4* fast = LDS_SCENE ? smem + 2 * n_nodes : uniform_ptr(w.leaf_fast);
     const int lane = threadIdx.x & 63;
-    unsigned long long todo = __ballot(T.phase == PH_TRACE && (T.fast & RTW_TF_SAH) != 0);
+    const uint4* keys = uniform_ptr(w.leaf_key);
     while (todo) {  // wave-uniform: one ray at a time
         const int src = __ffsll((long long)todo) - 1;
         todo &= todo - 1;
@@ -1432,6 +1443,7 @@ __device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, i
         r.o = v3(__shfl(T.ray.o.x, src), __shfl(T.ray.o.y, src), __shfl(T.ray.o.z, src));
         r.d = v3(__shfl(T.ray.d.x, src), __shfl(T.ray.d.y, src), __shfl(T.ray.d.z, src));
         r.time = __shfl(T.ray.time, src);
+        const int32_t sgn = __shfl(T.fast, src);  // bits 0-2: ray.d[axis] > 0
         float best = F32_INF;
         int32_t bl = -1;
         uint32_t cnt = 0;  // leaves of this lane reporting exactly `best`
@@ -1460,8 +1472,25 @@ __device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, i
 #pragma unroll
         for (int k = 1; k < 64; k <<= 1) m = rtw_minr(m, __shfl_xor(m, k));
         const unsigned long long at = __ballot(bl >= 0 && best == m);
-        const bool tie = __popcll(at) >= 2 || __ballot(bl >= 0 && best == m && cnt >= 2) != 0;
-        const int win = at ? __ffsll((long long)at) - 1 : 0;
+        bool tie = __ballot(bl >= 0 && best == m && cnt >= 2) != 0;
+        int win = at ? __ffsll((long long)at) - 1 : 0;
+        if (__popcll(at) >= 2) {  // one tied leaf per lane: the first in the reference's DFS order
+            if (keys) {
+                uint32_t k = 0xFFFFFFFFu;
+                if ((at >> lane) & 1) {
+                    const uint4 q = keys[bl];
+                    // bit = side XOR (the right child is visited first: ray.d[axis] <= 0)
+                    k = q.x ^ ((sgn & 1) ? 0u : q.y) ^ ((sgn & 2) ? 0u : q.z) ^ ((sgn & 4) ? 0u : q.w);
+                    if (audit) k = ~k;
+                }
+                uint32_t km = k;
+#pragma unroll
+                for (int j = 1; j < 64; j <<= 1) km = min(km, (uint32_t)__shfl_xor((int)km, j));
+                win = __ffsll((long long)__ballot(((at >> lane) & 1) && k == km)) - 1;
+            } else {
+                tie = true;
+            }
+        }
         const int32_t found = at ? __shfl(bl, win) : -1;
         if (lane == src) {
             T.found = found;
@@ -1776,7 +1805,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 wx_t0 = wx_tc;
 #endif
                 if (tm != 0 && (uint32_t)__popcll(tm) <= (uint32_t)A.coop_max)
-                    T = coop_trace<LDS, LK>(A.wdev, T, A.node_count, A.leaf_count, A.rect_count);
+                    T = coop_trace<LDS, LK>(A.wdev, T, tm, A.node_count, A.leaf_count, A.rect_count, A.coop_ties == 2);
             }
 #ifdef RTW_WAVE_TIMING
             const uint64_t wx_t1 = wall_clock64();
@@ -1795,6 +1824,12 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             // and hit_cond is monotone under box inclusion and in te, so L's parent box passing
             // hit_cond with te = succ(t) proves it.  A miss is a miss for the reference too.
             // Otherwise the ray is traced again on the reference tree.
+            // walk ties: coop_trace finds every tied leaf and keeps the reference's (its DFS-first)
+            if (!STATS && LK <= LK_PLAIN && A.coop_ties) {
+                const unsigned long long tl =
+                    __ballot(T.phase == PH_SHADE && (T.fast & (RTW_TF_SAH | RTW_TF_TIE)) == (RTW_TF_SAH | RTW_TF_TIE));
+                if (tl) T = coop_trace<LDS, LK>(A.wdev, T, tl, A.node_count, A.leaf_count, A.rect_count, A.coop_ties == 2);
+            }
             if (T.phase == PH_SHADE && (T.fast & RTW_TF_SAH)) {
                 bool ok = (T.fast & RTW_TF_TIE) == 0;
 #ifdef RTW_SAH_AUDIT_NO_TIE  // audit builds only: shows that the tie test decides images
@@ -2295,6 +2330,7 @@ struct SahTables {
     std::vector<float4> a, b;     // nodes, as node_a / node_b
     std::vector<float> km;        // cull constants, 2 per node
     std::vector<float4> box;      // 2 per leaf: the proof box (the leaf's parent box in the reference tree)
+    std::vector<uint4> key;       // per leaf: its DFS key material (DWorld::leaf_key), empty if too deep
     int32_t root = 0, depth = 0;
     bool ok = false;
 };
@@ -2364,6 +2400,39 @@ SahTables build_sah_tables(const rtw_world* w) {
         const rtw_bvh_node& p = w->nodes[parent[(size_t)i]];
         S.box[2 * (size_t)i] = make_float4(p.min[0], p.min[1], p.min[2], p.max[0]);
         S.box[2 * (size_t)i + 1] = make_float4(p.max[1], p.max[2], 0.0f, 0.0f);
+    }
+    // DFS keys: hittable.rs:441-445 visits the left child first when ray.d[axis] > 0, else the right
+    // one; a leaf's place in that order is the string of its ancestors' decisions (root first)
+    {
+        S.key.assign((size_t)L, make_uint4(0, 0, 0, 0));
+        bool ok = true;
+        struct Item { int32_t node; int depth; uint32_t side, a0, a1, a2; };
+        std::vector<Item> st{{w->root, 0, 0, 0, 0, 0}};
+        while (!st.empty() && ok) {
+            const Item it = st.back();
+            st.pop_back();
+            if (it.node < 0) {
+                S.key[(size_t)(-1 - it.node)] = make_uint4(it.side, it.a0, it.a1, it.a2);
+                continue;
+            }
+            if (it.depth >= 32) {
+                ok = false;
+                break;
+            }
+            const rtw_bvh_node& nd = w->nodes[it.node];
+            const uint32_t bit = 1u << (31 - it.depth);
+            Item c = it;
+            c.depth = it.depth + 1;
+            if (nd.axis == 0) c.a0 |= bit;
+            else if (nd.axis == 1) c.a1 |= bit;
+            else c.a2 |= bit;
+            c.node = nd.left;
+            st.push_back(c);
+            c.node = nd.right;
+            c.side |= bit;
+            st.push_back(c);
+        }
+        if (!ok) S.key.clear();
     }
     S.ok = true;
     return S;
@@ -2598,6 +2667,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     const size_t o_sb = sah.ok ? L.push(sah.b.data(), sah.b.size() * sizeof(float4)) : 0;
     const size_t o_sk = sah.ok ? L.push(sah.km.data(), sah.km.size() * sizeof(float)) : 0;
     const size_t o_lb = sah.ok ? L.push(sah.box.data(), sah.box.size() * sizeof(float4)) : 0;
+    const size_t o_lk = sah.ok && !sah.key.empty() ? L.push(sah.key.data(), sah.key.size() * sizeof(uint4)) : 0;
     WorldConst wcst;
     std::memset(&wcst, 0, sizeof(wcst));
     wcst.cam = w->camera;
@@ -2647,6 +2717,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         d.sah_b = (const float4*)(base + o_sb);
         d.sah_km = (const float2*)(base + o_sk);
         d.leaf_box = (const float4*)(base + o_lb);
+        d.leaf_key = o_lk ? (const uint4*)(base + o_lk) : nullptr;
         d.sah_root = sah.root;
     }
     d.has_light = w->has_light;
@@ -2820,6 +2891,11 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     A.coop_max = g->leaf_count <= RTW_COOP_LEAVES ? (int32_t)env_size("RTW_COOP_MAX", RTW_COOP_MAX) : 0;
     if (const char* e = std::getenv("RTW_COOP_MAX"))
         if (e[0] == '0') A.coop_max = 0;
+    A.coop_ties = g->leaf_count <= RTW_COOP_LEAVES && g->w.leaf_key != nullptr ? 1 : 0;
+    if (const char* e = std::getenv("RTW_COOP_TIES"))
+        if (e[0] == '0') A.coop_ties = 0;
+    if (const char* e = std::getenv("RTW_COOP_AUDIT"))  // tests only: the DFS-last tied leaf
+        if (e[0] == '1' && A.coop_ties) A.coop_ties = 2;
     A.node_count = sah ? g->sah_nodes : g->node_count;
     const size_t scene_bytes =
         (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);

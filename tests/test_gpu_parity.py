@@ -239,6 +239,33 @@ def test_sah_ties_and_grazing_hits(monkeypatch):
     assert_bit_identical(sah, R.render(big, 1, 4, 50, world, seed=31), "tie world, SAH vs reference tree")
 
 
+def test_coop_tie_resolution_decides_images(monkeypatch):
+    """the wave-cooperative trace finds every tied leaf and keeps the one the reference's
+    DFS visits first (leaf_key); the walk's tied rays and the drain's rays go through it.  Bit-exact
+    against the oracle and with the resolution off (re-traced on the reference tree), and an audit
+    setting that keeps the DFS-last tied leaf changes the image (the resolution decides pixels)."""
+    world = _tie_world()
+    dw = R.DeviceWorld(world, 0)
+    assert _kernel_tree(world) == "sah"
+    import torch
+
+    out = torch.empty(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
+    dw.render_into(R.render_params(R.Size2i(16, 16), 1, 50), out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert dw.kernel_variant()["leaf_kinds"] <= 2  # plain spheres / rects / triangles: coop_trace applies
+    size = R.Size2i(160, 90)
+    gpu = R.render(size, 1, 8, 50, world, seed=41)
+    assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=41)), "tie world, coop ties")
+    monkeypatch.setenv("RTW_COOP_TIES", "0")
+    monkeypatch.setenv("RTW_COOP_MAX", "0")
+    assert_bit_identical(gpu, R.render(size, 1, 8, 50, world, seed=41), "tie world, coop off")
+    monkeypatch.delenv("RTW_COOP_TIES")
+    monkeypatch.delenv("RTW_COOP_MAX")
+    monkeypatch.setenv("RTW_COOP_AUDIT", "1")
+    wrong = R.render(size, 1, 8, 50, world, seed=41)
+    assert not np.array_equal(np.asarray(wrong), np.asarray(gpu)), "the DFS-last tied leaf gave the same image"
+
+
 def test_progress_callback_reports_and_keeps_bits(worlds):
     """rtw_render_progress (the reference's progress thread, rendering.rs:140-157): monotone
     (done, total) reports ending at total, and the image equals rtw_render's."""
