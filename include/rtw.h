@@ -321,6 +321,15 @@ RTW_API int rtw_device_eval_node_pass(int device, const float* box, const float*
  * it: out[i] = 1 if RN(RN(sinf(x) sinf(y)) sinf(z)) < 0 for (x, y, z) = xyz[3i..3i+2], else 0. */
 RTW_API int rtw_device_eval_checker(int device, const float* xyz, int64_t n, int32_t* out);
 
+/* Device self-check of the exact fast divisions of the render kernel, counted on
+ * the device over n cases: test 0 the refined hardware reciprocal against 1/b for b = bits(base + i);
+ * test 1 division by pi and tau for a = bits(base + i); test 2 Markstein's correction on random
+ * pairs inside its guards; test 3 the guarded division helpers on random pairs of any kind (zeros,
+ * subnormals, extremes, infinities, NaN).  *mismatches = cases whose bits differ from IEEE division
+ * (NaN = NaN), *first = the first such i (~0 if none). */
+RTW_API int rtw_device_check_division(int device, int test, uint64_t base, uint64_t n, uint64_t seed,
+                                      uint64_t* mismatches, uint64_t* first);
+
 /* ---- host scene construction ------------------------------------------------------------- */
 typedef struct rtw_builder rtw_builder;         /* WorldBuilder + arena (world_builder.rs:7-14) */
 typedef struct rtw_world_handle rtw_world_handle; /* owns a finished flat World */

@@ -258,6 +258,10 @@ _SIGS = {
         [C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_float)],
     ),
     "rtw_device_eval_checker": (C.c_int, [C.c_int, C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_int32)]),
+    "rtw_device_check_division": (
+        C.c_int,
+        [C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)],
+    ),
     "rtw_device_eval_node_pass": (
         C.c_int,
         [C.c_int] + [C.POINTER(C.c_float)] * 4 + [C.c_int32, C.c_int64, C.POINTER(C.c_int32)],

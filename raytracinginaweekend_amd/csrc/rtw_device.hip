@@ -244,6 +244,80 @@ __host__ __device__ __forceinline__ V3 cross(V3 a, V3 b) {
 }
 __host__ __device__ __forceinline__ float len(V3 a) { return __builtin_sqrtf(dot(a, a)); }
 __host__ __device__ __forceinline__ V3 unit(V3 a) { return mul(a, 1.0f / len(a)); }  // vec3.rs:205-210
+// ---------------------------------------------------------------------------------------------
+// Exact divisions without the IEEE division sequence.  The compiler's correctly
+// rounded a / b is 11 VALU instructions (v_div_scale x2, v_rcp, 5 fma, v_div_fmas, v_div_fixup);
+// these give the same bits in 3 or 4 where a correctly rounded reciprocal is at hand.
+// rcp_nr(b): the hardware reciprocal (within 1 ulp) and one fma Newton step.  It equals IEEE 1 / b
+// for every f32 with 2^-100 <= |b| <= 2^100 (exhaustive on the device, rtw_device_check_division
+// test 0, tests/test_gpu_division.py); callers guard that range.
+#define RTW_RCP_LO 0x1p-100f
+#define RTW_RCP_HI 0x1p100f
+__device__ __forceinline__ float rcp_nr(float b) {
+    const float y = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
+}
+// RN(1 / b) for any b: the IEEE division outside rcp_nr's range (a rare, divergent branch)
+__device__ __forceinline__ float rcp_x(float b) {
+    float y = rcp_nr(b);
+    const float ab = __builtin_fabsf(b);
+    if (__builtin_expect(!(ab >= RTW_RCP_LO && ab <= RTW_RCP_HI), 0)) y = 1.0f / b;
+    return y;
+}
+// Markstein's correction (Markstein 1990): with y = RN(1/b), q = RN(a y), r = fma(-b, q, a) is exact
+// and RN(q + r y) = RN(a / b), provided 2^-22 <= |b| <= 2^22 and 2^-80 <= |a| <= 2^80 (no
+// intermediate underflows; tests/native/markstein_check.c range 2).  A zero a gives q = RN(a y) =
+// a / b exactly (the correction step could flip the sign of that zero, so it is not taken).
+#define RTW_MKA_LO 0x1p-80f
+#define RTW_MKA_HI 0x1p80f
+#define RTW_MKB_LO 0x1p-22f
+#define RTW_MKB_HI 0x1p22f
+__device__ __forceinline__ float mk_corr(float a, float b, float y) {
+    const float q = a * y;
+    return __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
+}
+__device__ __forceinline__ bool mk_a_ok(float a) {
+    const float x = __builtin_fabsf(a);
+    return x >= RTW_MKA_LO && x <= RTW_MKA_HI;
+}
+// RN(a / b) given y = RN(1 / b) with 2^-22 <= |b| <= 2^22 (the caller's guarantee)
+__device__ __forceinline__ float div_y(float a, float b, float y) {
+    float q = mk_corr(a, b, y);
+    if (__builtin_expect(!mk_a_ok(a), 0)) q = a / b;
+    return q;
+}
+// RN(a / b) for any a, b (IEEE where the guards fail)
+__device__ __forceinline__ float div_x(float a, float b) {
+    const float y = rcp_nr(b);
+    float q = mk_corr(a, b, y);
+    const float ab = __builtin_fabsf(b);
+    if (__builtin_expect(!(mk_a_ok(a) && ab >= RTW_MKB_LO && ab <= RTW_MKB_HI), 0)) q = a / b;
+    return q;
+}
+// a / s per component, y = RN(1 / s), 2^-22 <= |s| <= 2^22; one guard for the three dividends
+__device__ __forceinline__ V3 divs_y(V3 a, float s, float y) {
+    V3 q = v3(mk_corr(a.x, s, y), mk_corr(a.y, s, y), mk_corr(a.z, s, y));
+    const float lo = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+    const float hi = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+    if (__builtin_expect(!(lo >= RTW_MKA_LO && hi <= RTW_MKA_HI), 0)) q = divs(a, s);
+    return q;
+}
+__device__ __forceinline__ V3 divs_x(V3 a, float s) {
+    const float as = __builtin_fabsf(s);
+    if (__builtin_expect(!(as >= RTW_MKB_LO && as <= RTW_MKB_HI), 0)) return divs(a, s);
+    return divs_y(a, s, rcp_nr(s));
+}
+// Vec3::unit (vec3.rs:205-210): v * (1 / len)
+__device__ __forceinline__ V3 unit_x(V3 a) { return mul(a, rcp_x(len(a))); }
+// a / c for a positive constant c with yc = RN(1 / c) (constant-folded), 2^-22 <= c <= 2^22: a zero
+// a keeps its sign through q = a yc
+__device__ __forceinline__ float div_c(float a, float c, float yc) {
+    const float q = a * yc;
+    float r = __builtin_fmaf(__builtin_fmaf(-c, q, a), yc, q);
+    r = a == 0.0f ? q : r;
+    if (__builtin_expect(!(a == 0.0f || mk_a_ok(a)), 0)) r = a / c;
+    return r;
+}
 __device__ __forceinline__ float comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 __device__ __forceinline__ void setc(V3& a, int i, float v) {
     if (i == 0) a.x = v;
@@ -358,6 +432,19 @@ __device__ __forceinline__ bool rect_t(const RectG& g, const Ray& r, float ts, f
     return a >= g.r00 && a <= g.r01 && b >= g.r10 && b <= g.r11;
 }
 
+// the same for a Markstein-exact ray (RayPre::fast, §5.1) with y = RN(1 / d): every rect's dist
+// admits the guard like a node coordinate (mk_world), so t = RN((dist - o_n) / d_n) exactly; a zero
+// quotient may carry the other sign, and t = +-0 < ts = 0.001 is rejected either way
+__device__ __forceinline__ bool rect_t_mk(const RectG& g, const Ray& r, V3 inv, float ts, float te, float& t) {
+    int p0, p1, n;
+    rect_axes(g.plane, p0, p1, n);
+    t = mk_corr(g.dist - comp(r.o, n), comp(r.d, n), comp(inv, n));
+    if (!contains(ts, te, t)) return false;
+    const V3 pos = add(r.o, mul(r.d, t));
+    const float a = comp(pos, p0), b = comp(pos, p1);
+    return a >= g.r00 && a <= g.r01 && b >= g.r10 && b <= g.r11;
+}
+
 // aabb.rs:103-167
 __device__ __forceinline__ bool box_line(float4 ba, float4 bb, const Ray& r, float& nt, int& np, float& ft, int& fp) {
     const V3 mn = sub(v3(ba.x, ba.y, ba.z), r.o);
@@ -407,6 +494,7 @@ __device__ __forceinline__ bool box_t(const DWorld& w, int i, const Ray& r, floa
 struct TriFast {
     V3 p0, n, vt1, vt2;
     float den1, den2;
+    float y1, y2;  // RN(1 / den) when 2^-22 <= |den| <= 2^22, else 0 (div_tri then divides)
 };
 __host__ __device__ __forceinline__ TriFast tri_prepare(V3 p0, V3 p1, V3 p2) {
     TriFast f;
@@ -418,9 +506,15 @@ __host__ __device__ __forceinline__ TriFast tri_prepare(V3 p0, V3 p1, V3 p2) {
     f.den1 = dot(dir1, f.vt1);
     f.vt2 = cross(f.n, dir1);
     f.den2 = dot(dir2, f.vt2);
+    auto recip = [](float d) {
+        const float a = d < 0.0f ? -d : d;
+        return (a >= 0x1p-22f && a <= 0x1p22f) ? 1.0f / d : 0.0f;
+    };
+    f.y1 = recip(f.den1);
+    f.y2 = recip(f.den2);
     return f;
 }
-// 4 float4 per triangle: {p0.xyz, n.x} {n.yz, vt1.xy} {vt1.z, den1, vt2.xy} {vt2.z, den2, 0, 0}
+// 4 float4 per triangle: {p0.xyz, n.x} {n.yz, vt1.xy} {vt1.z, den1, vt2.xy} {vt2.z, den2, y1, y2}
 __device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i) {
     const float4 a = tf[4 * i], b = tf[4 * i + 1], c = tf[4 * i + 2], d = tf[4 * i + 3];
     TriFast f;
@@ -430,7 +524,15 @@ __device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i
     f.den1 = c.y;
     f.vt2 = v3(c.z, c.w, d.x);
     f.den2 = d.y;
+    f.y1 = d.z;
+    f.y2 = d.w;
     return f;
+}
+// a barycentric quotient a / den with the record's y = RN(1 / den) (0: den out of range)
+__device__ __forceinline__ float div_tri(float a, float den, float y) {
+    float q = mk_corr(a, den, y);
+    if (__builtin_expect(!(mk_a_ok(a) && y != 0.0f), 0)) q = a / den;
+    return q;
 }
 // a wave-uniform pointer in scalar registers
 template <class T>
@@ -449,12 +551,23 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
 __device__ __forceinline__ bool tri_test(const TriFast& T, const Ray& r, float ts, float te, float& t) {
     const float denom = dot(r.d, T.n);
     if (!(__builtin_fabsf(denom) > 0.0001f)) return false;
+    // t keeps the IEEE division: its divisor is ray-dependent, and rcp_nr + the correction + the
+    // dividend guard cost suzanne 3 % against it (register pressure in the leaf body;
+    // profiles/r03/v5_division_ab.txt)
     t = RTW_TDIV(dot(sub(T.p0, r.o), T.n), denom);
     if (!contains(ts, te, t)) return false;
     const V3 q = sub(at(r, t), T.p0);
+#ifdef RTW_EXP_FASTDIV_TRI
     const float w1 = RTW_TDIV(dot(q, T.vt1), T.den1);
+#else
+    const float w1 = div_tri(dot(q, T.vt1), T.den1, T.y1);
+#endif
     if (!(w1 > 0.0f && w1 < 1.0f)) return false;
+#ifdef RTW_EXP_FASTDIV_TRI
     const float w2 = RTW_TDIV(dot(q, T.vt2), T.den2);
+#else
+    const float w2 = div_tri(dot(q, T.vt2), T.den2, T.y2);
+#endif
     const float w0 = 1.0f - w1 - w2;
     return w2 > 0.0f && w0 > 0.0f;
 }
@@ -588,15 +701,15 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         const float4 s = (S.fast >= 0 && (flags & (RTW_LEAF_TRANSFORM | RTW_LEAF_ANIMATION)) == 0)
                              ? smem[S.fast + leaf] : w.spheres[idx];
         const V3 pos = at(rr, t);
-        const V3 sn = divs(sub(pos, v3(s.x, s.y, s.z)), s.w);
+        const V3 sn = divs_x(sub(pos, v3(s.x, s.y, s.z)), s.w);
         // uv (vec3.rs:241-249) only reaches the image through an image texture; a pure function
         // of the normal, so skipping it where no image texture can read it changes nothing
         float u = 0.0f, v = 0.0f;
         if (flags & RTW_DLEAF_UV) {
             const float theta = d_acosf(sn.y);
             const float phi = d_atan2f(-sn.z, sn.x) + F32_PI;
-            u = phi / F32_TAU;
-            v = theta / F32_PI;
+            u = div_c(phi, F32_TAU, 1.0f / F32_TAU);
+            v = div_c(theta, F32_PI, 1.0f / F32_PI);
         }
         from_ray(h, rr, pos, sn, u, v);
     } else if (kind == RTW_GEOM_RECT) {  // rect_geometry.rs:37-55
@@ -604,8 +717,8 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         int p0, p1, n;
         rect_axes(g.plane, p0, p1, n);
         const V3 pos = add(rr.o, mul(rr.d, t));
-        const float u = (comp(pos, p0) - g.r00) / (g.r01 - g.r00);
-        const float v = (comp(pos, p1) - g.r10) / (g.r01 - g.r10);  // the :45 typo
+        const float u = div_x(comp(pos, p0) - g.r00, g.r01 - g.r00);
+        const float v = div_x(comp(pos, p1) - g.r10, g.r01 - g.r10);  // the :45 typo
         V3 sn = v3(0.0f, 0.0f, 0.0f);
         setc(sn, n, -1.0f);
         from_ray(h, rr, pos, sn, u, v);
@@ -625,8 +738,8 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         const TriFast T = load_tri(w.tri_fast, idx);
         const V3 pos = at(rr, t);
         const V3 q = sub(pos, T.p0);
-        const float w1 = dot(q, T.vt1) / T.den1;
-        const float w2 = dot(q, T.vt2) / T.den2;
+        const float w1 = div_tri(dot(q, T.vt1), T.den1, T.y1);
+        const float w2 = div_tri(dot(q, T.vt2), T.den2, T.y2);
         const float w0 = 1.0f - w1 - w2;
         const float4 a0 = w.tri_attr[4 * idx], a1 = w.tri_attr[4 * idx + 1], a2 = w.tri_attr[4 * idx + 2],
                      a3 = w.tri_attr[4 * idx + 3];
@@ -692,11 +805,13 @@ struct RayPre {  // per-ray constants of the slab test
 // mk_world: every node coordinate is 0 or >= 2^-60 in magnitude (rtw_world_upload)
 __device__ __forceinline__ RayPre ray_pre(const Ray& r, bool mk_world) {
     RayPre p;
-    p.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
                                     __builtin_fabsf(r.d.z));
     const float M = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
                                     __builtin_fabsf(r.d.z));
+    // RN(1 / d) by rcp_nr inside its range (§5.8); zero or extreme components divide
+    p.inv = v3(rcp_nr(r.d.x), rcp_nr(r.d.y), rcp_nr(r.d.z));
+    if (__builtin_expect(!(m >= RTW_RCP_LO && M <= RTW_RCP_HI), 0)) p.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     p.fast = mk_world && (m >= RTW_MK_DMIN) && (M <= 2.0f) && mk_coord_ok(r.o.x) && mk_coord_ok(r.o.y) &&
              mk_coord_ok(r.o.z);
     return p;
@@ -941,7 +1056,7 @@ __device__ __forceinline__ V3 light_generate(const rtw_rect& g, V3 origin, rtw_x
     setc(e, p0, rtw_gen_range_f32(g.r0[0], g.r0[1], &rng));
     setc(e, p1, rtw_gen_range_f32(g.r1[0], g.r1[1], &rng));
     setc(e, n, g.dist);
-    return unit(sub(e, origin));
+    return unit_x(sub(e, origin));
 }
 __device__ __forceinline__ float light_value(const rtw_rect& lg, V3 origin, V3 dir) {
     Ray r;
@@ -960,7 +1075,7 @@ __device__ __forceinline__ float light_value(const rtw_rect& lg, V3 origin, V3 d
     const float area = (g.r01 - g.r00) * (g.r11 - g.r10);
     const float dsq = t * t;
     const float cosine = __builtin_fabsf(dot(hn, dir));
-    return dsq / (cosine * area);
+    return div_x(dsq, cosine * area);
 }
 
 // background_color.rs:9-19; `pdot` = dot((0, 1, 0), d) of the primary ray, computed once per sample
@@ -987,7 +1102,7 @@ __device__ __forceinline__ Ray camera_ray(const rtw_camera& c, rtw_xoro& rng, fl
     Ray r;
     r.time = start + (c.shutter_pace[0] * px + c.shutter_pace[1] * py);
     r.o = add(ld3(c.position), off);
-    r.d = unit(sub(sub(add(ld3(c.upper_left_corner), mul(ld3(c.scaled_right), px)), mul(ld3(c.scaled_up), py)), off));
+    r.d = unit_x(sub(sub(add(ld3(c.upper_left_corner), mul(ld3(c.scaled_right), px)), mul(ld3(c.scaled_up), py)), off));
     return r;
 }
 
@@ -1056,26 +1171,26 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                     }
                     const V3 dir = add(reflect(ray.d, h.n), fz);
                     if (dot(dir, h.n) > 0.0f) {
-                        sdir = unit(dir);
+                        sdir = unit_x(dir);
                         tex = M.y;
                     } else {
                         scatters = false;
                     }
                 } else if (mkind == RTW_MAT_DIELECTRIC) {
                     const float ior = __int_as_float(M.w);
-                    const float ratio = h.front ? (1.0f / ior) : ior;
+                    const float ratio = h.front ? rcp_x(ior) : ior;
                     const float cos_t = rtw_minr(dot(neg(ray.d), h.n), 1.0f);
                     const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
                     bool refl = ratio * sin_t > 1.0f;
                     if (!refl) {
-                        const float r0 = (1.0f - ratio) / (1.0f + ratio);
+                        const float r0 = div_x(1.0f - ratio, 1.0f + ratio);
                         const float rs = r0 * r0;
                         const float x = 1.0f - cos_t;
                         const float x2 = x * x;
                         const float p5 = x * (x2 * x2);  // powi(5)
                         refl = (rs + (1.0f - rs) * p5) > rtw_gen_f32(&rng);
                     }
-                    sdir = unit(refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio));
+                    sdir = unit_x(refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio));
                 } else if (mkind == RTW_MAT_ISOTROPIC) {
                     need_sphere = true;
                     tex = M.y;
@@ -1098,7 +1213,12 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                     if (cosine) {  // (n + UnitSphere).unit_or_else(n) (material.rs:20-22)
                         const V3 v = add(h.n, sv);
                         const float lsq = dot(v, v);
-                        sdir = (lsq > 1e-8f) ? divs(v, __builtin_sqrtf(lsq)) : h.n;
+                        if (lsq > 1e-8f) {  // 1e-4 < s <= 2: inside div_y's divisor range
+                            const float s = __builtin_sqrtf(lsq);
+                            sdir = divs_y(v, s, rcp_nr(s));
+                        } else {
+                            sdir = h.n;
+                        }
                     } else {
                         sdir = sv;
                     }
@@ -1109,11 +1229,16 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                 if (scatters) {
                     float prob = 1.0f;
                     if (cosine) {
-                        const float mv = rtw_maxr(dot(h.n, sdir), 0.0f) / F32_PI;  // Cosine::value
-                        float p = mv;
-                        if (w.has_light) p = 0.5f * light_value(w.wc->light, h.pos, sdir) + (1.0f - 0.5f) * mv;
-                        const float spdf = rtw_maxr(dot(h.n, sdir), 0.0f) / F32_PI;  // material.rs:123-127
-                        prob = spdf / p;
+                        const float mv = div_c(rtw_maxr(dot(h.n, sdir), 0.0f), F32_PI, 1.0f / F32_PI);  // Cosine::value
+                        // material.rs:123-127: the same expression as mv, so without a light p = spdf
+                        // and spdf / p is 1 (finite non-zero spdf) or 0 / 0
+                        const float spdf = mv;
+                        if (w.has_light) {
+                            const float p = 0.5f * light_value(w.wc->light, h.pos, sdir) + (1.0f - 0.5f) * mv;
+                            prob = div_x(spdf, p);
+                        } else {
+                            prob = spdf != 0.0f ? 1.0f : __builtin_nanf("");
+                        }
                     }
                     acc = add(acc, conv(att, emitted));
                     att = mul(conv(att, albedo), prob);
@@ -1323,7 +1448,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
                 float t;
                 V3 pos;
-                if (rect_t(g, T.ray, 0.001f, T.te, t, pos)) take(t, leaf);
+                if (FAST_ONLY ? rect_t_mk(g, T.ray, rp.inv, 0.001f, T.te, t) : rect_t(g, T.ray, 0.001f, T.te, t, pos))
+                    take(t, leaf);
             } else if (LK == LK_TRIS || LK == LK_PLAIN || __float_as_int(sph.x) == 1) {  // a plain triangle
                 if (STATS) st.c[ST_T_TRI]++;
                 float t;
@@ -1443,6 +1569,7 @@ __device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, u
         r.o = v3(__shfl(T.ray.o.x, src), __shfl(T.ray.o.y, src), __shfl(T.ray.o.z, src));
         r.d = v3(__shfl(T.ray.d.x, src), __shfl(T.ray.d.y, src), __shfl(T.ray.d.z, src));
         r.time = __shfl(T.ray.time, src);
+        const V3 inv = v3(__shfl(T.inv.x, src), __shfl(T.inv.y, src), __shfl(T.inv.z, src));
         const int32_t sgn = __shfl(T.fast, src);  // bits 0-2: ray.d[axis] > 0
         float best = F32_INF;
         int32_t bl = -1;
@@ -1457,8 +1584,7 @@ __device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, u
                 const int ri = __float_as_int(sph.y);
                 const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
                 const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
-                V3 pos;
-                hit = rect_t(g, r, 0.001f, F32_INF, t, pos);
+                hit = rect_t_mk(g, r, inv, 0.001f, F32_INF, t);  // SAH rays are Markstein-exact
             } else {
                 hit = tri_test(load_tri(tri_fast, __float_as_int(sph.y)), r, 0.001f, F32_INF, t);
             }
@@ -2193,6 +2319,71 @@ __global__ void eval_node_pass_kernel(const float* box, const float* ray, const 
     out[i] = node_pass(na, nb, make_float2(km[2 * i], km[2 * i + 1]), R, rp, range[2 * i], range[2 * i + 1]) ? 1 : 0;
 }
 
+// Self-check of the exact fast divisions (§5.8) on the device, counted there.  Case i of [0, n):
+//   test 0: b = bits(base + i): rcp_nr(b) against 1 / b (the caller picks the exponent range)
+//   test 1: a = bits(base + i): div_c(a, pi), div_c(a, tau) against a / pi, a / tau (any a)
+//   test 2: a random pair inside Markstein's guards: mk_corr(a, b, rcp_nr(b)) against a / b
+//   test 3: a random pair of any kind (zeros, subnormals, extremes, inf, NaN): div_x, div_tri (y as
+//           tri_prepare sets it), rcp_x and divs_x's components against IEEE division
+// out[0] += mismatches, out[1] = min over mismatching i (the first one, ~0 if none)
+__device__ __forceinline__ uint64_t chk_mix(uint64_t x) {
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 27; x *= 0x94D049BB133111EBull; return x ^ (x >> 31);
+}
+__device__ __forceinline__ bool chk_same(float x, float y) { return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y); }
+__device__ __forceinline__ float chk_float(uint64_t r, int e_lo, int e_hi) {  // random sign / mantissa, exponent in [e_lo, e_hi]
+    const int e = e_lo + (int)((r >> 32) % (uint64_t)(e_hi - e_lo + 1));
+    return __uint_as_float((uint32_t)(r & 0x807FFFFFu) | ((uint32_t)(e + 127) << 23));
+}
+__device__ __forceinline__ float chk_any(uint64_t r) {  // special values, extremes and plain floats
+    switch ((r >> 56) & 15) {
+        case 0: return (r & 1) ? -0.0f : 0.0f;
+        case 1: return __uint_as_float((uint32_t)r & 0x807FFFFFu);  // subnormal
+        case 2: return chk_float(r, -126, -90);
+        case 3: return chk_float(r, 90, 127);
+        case 4: return (r & 1) ? -F32_INF : F32_INF;
+        case 5: return __uint_as_float(0x7FC00000u | ((uint32_t)r & 0x803FFFFFu));
+        case 6: return chk_float(r, -104, -76);  // the guards' edges
+        case 7: return chk_float(r, 76, 104);
+        case 8: return chk_float(r, -24, -20);
+        case 9: return chk_float(r, 20, 24);
+        default: return chk_float(r, -30, 30);
+    }
+}
+__global__ void check_division_kernel(int test, uint64_t base, uint64_t n, uint64_t seed, unsigned long long* out) {
+    uint64_t bad = 0, first = ~0ull;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        bool ok = true;
+        if (test == 0) {
+            const float b = __uint_as_float((uint32_t)(base + i));
+            ok = chk_same(rcp_nr(b), 1.0f / b);
+        } else if (test == 1) {
+            const float a = __uint_as_float((uint32_t)(base + i));
+            ok = chk_same(div_c(a, F32_PI, 1.0f / F32_PI), a / F32_PI) && chk_same(div_c(a, F32_TAU, 1.0f / F32_TAU), a / F32_TAU);
+        } else if (test == 2) {
+            const uint64_t r1 = chk_mix(seed ^ (2 * i)), r2 = chk_mix(seed ^ (2 * i + 1));
+            const float a = chk_float(r1, -80, 80), b = chk_float(r2, -22, 22);
+            ok = chk_same(mk_corr(a, b, rcp_nr(b)), a / b);
+        } else {
+            const uint64_t r1 = chk_mix(seed ^ (2 * i)), r2 = chk_mix(seed ^ (2 * i + 1));
+            const float a = chk_any(r1), b = chk_any(r2);
+            const float ab = __builtin_fabsf(b);
+            const float y = (ab >= 0x1p-22f && ab <= 0x1p22f) ? 1.0f / b : 0.0f;  // tri_prepare's rule
+            const V3 q = divs_x(v3(a, b, a * 0.5f), b), e = divs(v3(a, b, a * 0.5f), b);
+            ok = chk_same(div_x(a, b), a / b) && chk_same(div_tri(a, b, y), a / b) && chk_same(rcp_x(b), 1.0f / b) &&
+                 chk_same(q.x, e.x) && chk_same(q.y, e.y) && chk_same(q.z, e.z);
+        }
+        if (!ok) {
+            ++bad;
+            first = min(first, (unsigned long long)i);
+        }
+    }
+    if (bad) {
+        atomicAdd(&out[0], (unsigned long long)bad);
+        atomicMin(&out[1], (unsigned long long)first);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -2284,6 +2475,8 @@ int check_world(const rtw_world* w, int* depth_out) {
         if (big(w->nodes[i].min, 3) || big(w->nodes[i].max, 3)) return bad("node bounds beyond 2^30");
     for (int i = 0; i < w->sphere_count; ++i)
         if (big(w->spheres[i].center, 4)) return bad("sphere beyond 2^30");
+    for (int i = 0; i < w->rect_count; ++i)
+        if (big(&w->rects[i].dist, 1)) return bad("rect beyond 2^30");
     for (int i = 0; i < w->leaf_count; ++i) {
         const rtw_leaf& L = w->leaves[i];
         float vt[3];
@@ -2608,7 +2801,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         tp[4 * (size_t)i] = make_float4(f.p0.x, f.p0.y, f.p0.z, f.n.x);
         tp[4 * (size_t)i + 1] = make_float4(f.n.y, f.n.z, f.vt1.x, f.vt1.y);
         tp[4 * (size_t)i + 2] = make_float4(f.vt1.z, f.den1, f.vt2.x, f.vt2.y);
-        tp[4 * (size_t)i + 3] = make_float4(f.vt2.z, f.den2, 0.0f, 0.0f);
+        tp[4 * (size_t)i + 3] = make_float4(f.vt2.z, f.den2, f.y1, f.y2);
         const float (*n)[3] = t.normals;
         const float (*u)[2] = t.uvs;
         ta[4 * (size_t)i] = make_float4(n[0][0], n[0][1], n[0][2], n[1][0]);
@@ -2758,6 +2951,9 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         for (int k = 0; k < 3; ++k)
             for (float c : {w->nodes[i].min[k], w->nodes[i].max[k]})
                 if (!(c == 0.0f || std::fabs(c) >= 0x1p-60f)) g->mk_world = 0;
+    // rect planes: the Markstein rect test (rect_t_mk) divides dist - o_n like a node coordinate
+    for (int i = 0; i < w->rect_count; ++i)
+        if (!(w->rects[i].dist == 0.0f || std::fabs(w->rects[i].dist) >= 0x1p-60f)) g->mk_world = 0;
     // audits: RTW_NO_MARKSTEIN=1 makes every ray take the true-division slab test (and the traversal
     // loop that carries it)
     if (const char* e = std::getenv("RTW_NO_MARKSTEIN"))
@@ -3415,6 +3611,26 @@ extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, c
     (void)hipFree(dg);
     (void)hipFree(dk);
     (void)hipFree(dout);
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_device_check_division(int device, int test, uint64_t base, uint64_t n, uint64_t seed,
+                                                 uint64_t* mismatches, uint64_t* first) {
+    if (!mismatches || !first || test < 0 || test > 3) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device");
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 2 * sizeof(unsigned long long)));
+    const unsigned long long init[2] = {0ull, ~0ull};
+    HIP_TRY(hipMemcpy(d, init, sizeof(init), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(check_division_kernel, dim3(8192), dim3(256), 0, 0, test, base, n, seed, d);
+    HIP_TRY(hipGetLastError());
+    unsigned long long res[2];
+    HIP_TRY(hipMemcpy(res, d, sizeof(res), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    *mismatches = res[0];
+    *first = res[1];
     return RTW_OK;
 }
 

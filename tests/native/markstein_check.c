@@ -1,8 +1,10 @@
 /* Exhaustive-over-divisor check of the division used by the device slab tests
  * (rtw_device.hip mk_div / node_pass):
  *   y = RN(1/b); q = RN(a*y); r = fma(-b, q, a); q' = fma(r, y, q)
- * must equal RN(a/b) under the kernel's guards: 2^-60 <= |b| <= 2, 2^-84 <= |a| <= 2^40
- * (a = 0 gives a zero quotient whose sign may differ; no comparison of the slab test sees it).
+ * must equal RN(a/b) under the kernel's guards: range 1 (slab and rect tests, per-ray
+ * reciprocals) 2^-60 <= |b| <= 2, 2^-84 <= |a| <= 2^40 (a = 0 gives a zero quotient whose sign may
+ * differ; no comparison of the slab test sees it); range 2 (the shading and triangle divisions,
+ * DESIGN §5.8) 2^-22 <= |b| <= 2^22, 2^-80 <= |a| <= 2^80.
  * (Markstein 1990; Handbook of Floating-Point Arithmetic, Thm. "Markstein".)
  * For every divisor significand (2^23) and a spread of exponents, test many dividends. */
 #include <math.h>
@@ -22,10 +24,11 @@ int main(int argc, char** argv) {
     for (uint32_t m = 0; m < (1u << 23); ++m) {
         for (int k = 0; k < per; ++k) {
             const uint64_t r = nxt();
-            const int be = (int)(r % 62) - 60;                        /* divisor exponent in [-60, 1] */
+            const int r2 = (int)((r >> 60) & 1u);                     /* range 2 for every other case */
+            const int be = r2 ? (int)(r % 45) - 22 : (int)(r % 62) - 60; /* divisor exponent */
             const uint32_t bs = (uint32_t)((r >> 8) & 1u) << 31;
             const float b = u2f(bs | ((uint32_t)(be + 127) << 23) | m);
-            const int ae = (int)((r >> 9) % 124) - 84;                /* dividend exponent in [-84, 39] */
+            const int ae = r2 ? (int)((r >> 9) % 161) - 80 : (int)((r >> 9) % 124) - 84; /* dividend exponent */
             const uint32_t am = (uint32_t)(r >> 20) & 0x7FFFFFu;
             const uint32_t as = (uint32_t)((r >> 50) & 1u) << 31;
             const float a = u2f(as | ((uint32_t)(ae + 127) << 23) | am);
@@ -33,7 +36,8 @@ int main(int argc, char** argv) {
             const float q = a * y;
             const float rr = fmaf(-b, q, a);
             const float q2 = fmaf(rr, y, q);
-            if (fabsf(b) > 2.0f) { ++guarded_out; continue; }
+            if (!r2 && fabsf(b) > 2.0f) { ++guarded_out; continue; }
+            if (r2 && fabsf(b) > 0x1p22f) { ++guarded_out; continue; }
             const float t = a / b;
             ++tested;
             if (f2u(t) != f2u(q2)) {
