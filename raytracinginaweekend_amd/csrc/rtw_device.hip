@@ -307,8 +307,26 @@ __device__ __forceinline__ V3 divs_x(V3 a, float s) {
     if (__builtin_expect(!(as >= RTW_MKB_LO && as <= RTW_MKB_HI), 0)) return divs(a, s);
     return divs_y(a, s, rcp_nr(s));
 }
+// Correctly rounded sqrt without the compiler's range handling: v_sqrt_f32 and the +-1 ulp
+// correction by two fma residuals, the compiler's own sequence minus the scaling of inputs below
+// 2^-96 and the zero / inf select.  Equal to sqrtf on every f32 in [2^-96, FLT_MAX] (exhaustive on
+// the device, rtw_device_check_division test 4).  sqrt_nr: the caller knows the range; sqrt_x: any x.
+#define RTW_SQRT_LO 0x1p-96f
+__device__ __forceinline__ float sqrt_nr(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
+    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+    float r = rm <= 0.0f ? sm : s;
+    r = rp > 0.0f ? sp : r;
+    return r;
+}
+__device__ __forceinline__ float sqrt_x(float x) {
+    float r = sqrt_nr(x);
+    if (__builtin_expect(!(x >= RTW_SQRT_LO && x <= 0x1.fffffep127f), 0)) r = __builtin_sqrtf(x);
+    return r;
+}
 // Vec3::unit (vec3.rs:205-210): v * (1 / len)
-__device__ __forceinline__ V3 unit_x(V3 a) { return mul(a, rcp_x(len(a))); }
+__device__ __forceinline__ V3 unit_x(V3 a) { return mul(a, rcp_x(sqrt_x(dot(a, a)))); }
 // a / c for a positive constant c with yc = RN(1 / c) (constant-folded), 2^-22 <= c <= 2^22: a zero
 // a keeps its sign through q = a yc
 __device__ __forceinline__ float div_c(float a, float c, float yc) {
@@ -329,7 +347,7 @@ __device__ __forceinline__ V3 reflect(V3 d, V3 n) { return sub(d, mul(n, 2.0f * 
 __device__ __forceinline__ V3 refract(V3 d, V3 n, float eta) {  // vec3.rs:235-240
     const float cos_theta = rtw_minr(dot(neg(d), n), 1.0f);
     const V3 perp = mul(add(d, mul(n, cos_theta)), eta);
-    const float k = -__builtin_sqrtf(__builtin_fabsf(1.0f - dot(perp, perp)));
+    const float k = -sqrt_x(__builtin_fabsf(1.0f - dot(perp, perp)));
     return add(perp, mul(n, k));
 }
 
@@ -394,7 +412,7 @@ __device__ __forceinline__ bool sphere_t(float4 s, const Ray& r, float ts, float
     const float c = dot(oc, oc) - s.w * s.w;
     const float disc = half_b * half_b - c;
     if (disc < 0.0f) return false;
-    const float sq = __builtin_sqrtf(disc);
+    const float sq = sqrt_x(disc);
     const float small = -half_b - sq;
     if (contains(ts, te, small)) {
         t = small;
@@ -1180,7 +1198,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                     const float ior = __int_as_float(M.w);
                     const float ratio = h.front ? rcp_x(ior) : ior;
                     const float cos_t = rtw_minr(dot(neg(ray.d), h.n), 1.0f);
-                    const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+                    const float sin_t = sqrt_x(1.0f - cos_t * cos_t);
                     bool refl = ratio * sin_t > 1.0f;
                     if (!refl) {
                         const float r0 = div_x(1.0f - ratio, 1.0f + ratio);
@@ -1214,7 +1232,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                         const V3 v = add(h.n, sv);
                         const float lsq = dot(v, v);
                         if (lsq > 1e-8f) {  // 1e-4 < s <= 2: inside div_y's divisor range
-                            const float s = __builtin_sqrtf(lsq);
+                            const float s = sqrt_nr(lsq);  // 1e-8 < lsq <= 4
                             sdir = divs_y(v, s, rcp_nr(s));
                         } else {
                             sdir = h.n;
@@ -2323,6 +2341,7 @@ __global__ void eval_node_pass_kernel(const float* box, const float* ray, const 
 //   test 0: b = bits(base + i): rcp_nr(b) against 1 / b (the caller picks the exponent range)
 //   test 1: a = bits(base + i): div_c(a, pi), div_c(a, tau) against a / pi, a / tau (any a)
 //   test 2: a random pair inside Markstein's guards: mk_corr(a, b, rcp_nr(b)) against a / b
+//   test 4: a = bits(base + i): sqrt_x (and sqrt_nr inside its range) against sqrtf
 //   test 3: a random pair of any kind (zeros, subnormals, extremes, inf, NaN): div_x, div_tri (y as
 //           tri_prepare sets it), rcp_x and divs_x's components against IEEE division
 // out[0] += mismatches, out[1] = min over mismatching i (the first one, ~0 if none)
@@ -2360,6 +2379,10 @@ __global__ void check_division_kernel(int test, uint64_t base, uint64_t n, uint6
         } else if (test == 1) {
             const float a = __uint_as_float((uint32_t)(base + i));
             ok = chk_same(div_c(a, F32_PI, 1.0f / F32_PI), a / F32_PI) && chk_same(div_c(a, F32_TAU, 1.0f / F32_TAU), a / F32_TAU);
+        } else if (test == 4) {
+            const float a = __uint_as_float((uint32_t)(base + i));
+            ok = chk_same(sqrt_x(a), __builtin_sqrtf(a));
+            if (a >= RTW_SQRT_LO && a <= 0x1.fffffep127f) ok = ok && chk_same(sqrt_nr(a), __builtin_sqrtf(a));
         } else if (test == 2) {
             const uint64_t r1 = chk_mix(seed ^ (2 * i)), r2 = chk_mix(seed ^ (2 * i + 1));
             const float a = chk_float(r1, -80, 80), b = chk_float(r2, -22, 22);
@@ -3616,7 +3639,7 @@ extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, c
 
 extern "C" RTW_API int rtw_device_check_division(int device, int test, uint64_t base, uint64_t n, uint64_t seed,
                                                  uint64_t* mismatches, uint64_t* first) {
-    if (!mismatches || !first || test < 0 || test > 3) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
+    if (!mismatches || !first || test < 0 || test > 4) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device");
     HIP_TRY(hipSetDevice(device));

@@ -4,7 +4,8 @@ The kernel replaces the 11-instruction correctly rounded f32 division with a ref
 reciprocal (v_rcp_f32 + one fma Newton step) and Markstein's correction wherever a correctly rounded
 reciprocal is at hand.  The reciprocal is a property of this hardware, so it is pinned exhaustively on
 the device: every f32 of its guarded range, both signs.  Division by the constants pi and tau is
-checked for every f32 dividend.  Markstein's correction (a published theorem) is sampled on 2^32
+checked for every f32 dividend, and the fast sqrt (v_sqrt_f32 + the ±1 ulp correction
+without the range handling) for every f32.  Markstein's correction (a published theorem) is sampled on 2^32
 pairs inside its guards, and the guarded helpers (their IEEE fallbacks included) on 2^30 pairs of any
 kind: zeros, subnormals, extremes, infinities and NaN.  Counting happens on the device
 (rtw_device_check_division); zero mismatches are required."""
@@ -49,3 +50,9 @@ def test_markstein_inside_guards():
 def test_guarded_helpers_any_input():
     bad, first = _check(3, 0, 1 << 30, seed=0xD1CE)
     assert bad == 0, f"{bad} mismatches, first case {first}"
+
+
+def test_sqrt_every_f32():
+    # sqrt_x on every bit pattern, sqrt_nr (no range handling) on [2^-96, FLT_MAX]
+    bad, first = _check(4, 0, 1 << 32)
+    assert bad == 0, f"sqrt_x / sqrt_nr differ from sqrtf on {bad} inputs, first bits {first:#010x}"
