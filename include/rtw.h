@@ -313,7 +313,8 @@ RTW_API int rtw_device_eval_scalar(int device, int fn, const float* a, const flo
  * (1: node coordinates admit the per-ray exact-division guard).  out[i] = 1 if the node passes.
  * mk_world = 2 evaluates the SAH walk's node test instead (one-multiply quotients,
  * constants widened x17/16 as uploaded) beside the cull alone with exact quotients: out[i] bit 0 =
- * SAH test passes, bit 1 = exact cull passes, bit 2 = the ray admits the exact division. */
+ * SAH test passes, bit 1 = exact cull passes, bit 2 = the ray admits the exact division.
+ * mk_world = 3: the same with the D^2 k term the render kernel uses (2: round 2's Dq form). */
 RTW_API int rtw_device_eval_node_pass(int device, const float* box, const float* ray, const float* range,
                                       const float* km, int32_t mk_world, int64_t n, int32_t* out);
 

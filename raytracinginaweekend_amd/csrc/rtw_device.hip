@@ -912,20 +912,26 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
 // lies outside the exact test's bound (RN is monotone), and this test passes every node that
 // test passes.  One multiply per quotient instead of three operations.
 #define RTW_SAH_WIDEN (17.0f / 16.0f)
+// DQ = false (the product): the k term takes D^2 >= Dq, so delta = fma(D, fma(k, D, 68u), m): two
+// operations for five, and a delta at least as large up to two roundings (the containment argument's
+// margin is 17/16 against 1 + 3/64; tests/test_gpu_node_pass.py checks both forms)
+template <bool DQ = true>
 __device__ __forceinline__ float sah_delta(float k, float m, float a0, float b0, float a1, float b1, float a2, float b2) {
     const float m0 = __builtin_fmaxf(__builtin_fabsf(a0), __builtin_fabsf(b0));
     const float m1 = __builtin_fmaxf(__builtin_fabsf(a1), __builtin_fabsf(b1));
     const float m2 = __builtin_fmaxf(__builtin_fabsf(a2), __builtin_fabsf(b2));
     const float d = (m0 + m1) + m2;
+    if (!DQ) return __builtin_fmaf(d, __builtin_fmaf(k, d, 64.0f * RTW_SAH_WIDEN * RTW_CULL_U), m);
     const float dq = __builtin_fmaf(m2, m2, __builtin_fmaf(m1, m1, m0 * m0));
     return __builtin_fmaf(k, dq, __builtin_fmaf(64.0f * RTW_SAH_WIDEN * RTW_CULL_U, d, m));
 }
+template <bool DQ = true>
 __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, const Ray& r, const RayPre& rp, float ts,
                                                float te, float& entry) {
     const float a0 = na.x - r.o.x, b0 = na.w - r.o.x;
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
-    const float delta = sah_delta(km.x, km.y, a0, b0, a1, b1, a2, b2);
+    const float delta = sah_delta<DQ>(km.x, km.y, a0, b0, a1, b1, a2, b2);
 #ifdef RTW_SAH_EXACT_Q  // audit / A/B builds: the exact quotients of the reference tree's test
     const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
     const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
@@ -1392,6 +1398,13 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // the pushed child's entry t, so that a pop skips children starting beyond te, lost 5 %: the
     // skip loop's divergence costs more than the node steps it saves, profiles/r02/v9_two_child_ab.txt.)
     constexpr bool C2 = TM == TM_SAH && LK == LK_SPHERES;
+    // the SAH node test's k term: D^2 (two operations; every world gained 0.5 %,
+    // profiles/r03/v6_delta_d2_ab.txt); RTW_SAH_DQ builds keep round 2's Dq form
+#ifdef RTW_SAH_DQ
+    constexpr bool SAH_DQ = true;
+#else
+    constexpr bool SAH_DQ = false;
+#endif
     auto pop = [&]() {
         if (T.sp == 0) T.phase = PH_SHADE;
         else T.node = stack[(--T.sp) * RTW_BLOCK];
@@ -1499,8 +1512,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             const float2 lk = nkm[il], rk = nkm[ir];
             float el, er;
             if (STATS) st.c[ST_NODES] += (left >= 0) + (right >= 0);  // the child boxes tested
-            const bool pl = node_pass_cons(la, lb, lk, T.ray, rp, 0.001f, T.te, el) || left < 0;
-            const bool pr = node_pass_cons(ra, rb, rk, T.ray, rp, 0.001f, T.te, er) || right < 0;
+            const bool pl = node_pass_cons<SAH_DQ>(la, lb, lk, T.ray, rp, 0.001f, T.te, el) || left < 0;
+            const bool pr = node_pass_cons<SAH_DQ>(ra, rb, rk, T.ray, rp, 0.001f, T.te, er) || right < 0;
             if (left < 0) el = -F32_INF;
             if (right < 0) er = -F32_INF;
             if (pl && pr) {
@@ -1520,7 +1533,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             const float4 nb = nodes_b[T.node];
             const float2 km = nkm[T.node];
             float entry;
-            if (TM == TM_SAH ? node_pass_cons(na, nb, km, T.ray, rp, 0.001f, T.te, entry)
+            if (TM == TM_SAH ? node_pass_cons<SAH_DQ>(na, nb, km, T.ray, rp, 0.001f, T.te, entry)
                              : node_pass<FAST_ONLY>(na, nb, km, T.ray, rp, 0.001f, T.te)) {
                 if (STATS) db[DB_PASS_LANES]++;
                 const int32_t lbits = __float_as_int(nb.z);
@@ -2318,9 +2331,9 @@ __global__ void eval_node_pass_kernel(const float* box, const float* ray, const 
     R.o = v3(r[0], r[1], r[2]);
     R.d = v3(r[3], r[4], r[5]);
     R.time = 0.0f;
-    const RayPre rp = ray_pre(R, mk_world != 0);
+    const RayPre rp = ray_pre(R, mk_world != 0);  // modes 2 and 3: the SAH tests (mk world)
     const float4 na = make_float4(b[0], b[1], b[2], b[3]), nb = make_float4(b[4], b[5], 0.0f, 0.0f);
-    if (mk_world == 2) {
+    if (mk_world == 2 || mk_world == 3) {
         // the SAH walk's node test (cheap quotients, constants widened as build_sah_tables uploads
         // them) beside the cull alone with exact quotients and the plain constants: bit 0 = SAH test
         // passes, bit 1 = exact cull passes, bit 2 = the ray is Markstein-exact (the SAH walk's rays)
@@ -2328,7 +2341,8 @@ __global__ void eval_node_pass_kernel(const float* box, const float* ray, const 
         if (k > 0.0f) k = nextafterf(k * RTW_SAH_WIDEN, F32_INF);
         if (m > 0.0f) m = nextafterf(m * RTW_SAH_WIDEN, F32_INF);
         float e;
-        const bool sah = node_pass_cons(na, nb, make_float2(k, m), R, rp, range[2 * i], range[2 * i + 1], e);
+        const bool sah = mk_world == 2 ? node_pass_cons<true>(na, nb, make_float2(k, m), R, rp, range[2 * i], range[2 * i + 1], e)
+                                       : node_pass_cons<false>(na, nb, make_float2(k, m), R, rp, range[2 * i], range[2 * i + 1], e);
         const bool exact = node_pass_cull_exact(na, nb, make_float2(km[2 * i], km[2 * i + 1]), R, rp, range[2 * i],
                                                 range[2 * i + 1]);
         out[i] = (sah ? 1 : 0) | (exact ? 2 : 0) | (rp.fast ? 4 : 0);

@@ -90,13 +90,14 @@ def test_sah_node_test_contains_exact_cull():
     """The SAH walk's node test (one-multiply quotients, cull constants widened x17/16 and a 68u D
     term, rtw_device.hip node_pass_cons) passes every node that the cull with exact quotients and
     the plain constants passes, on every ray the SAH walk traces (Markstein-exact rays): DESIGN.md
-    §5.5's containment argument, checked on 2 M random and special-value cases."""
-    for seed in (21, 22):
+    §5.5's containment argument, checked on 2 M random and special-value cases; for both forms of the
+    delta's k term (mode 2: Dq, round 2's form; mode 3: D^2, the product's)."""
+    for seed, mode in ((21, 2), (22, 2), (23, 3), (24, 3)):
         rng = np.random.default_rng(seed)
         box, ray, rg, km = _cases(rng, 1_000_000, True)
         k = km[:, 0]
         km[:, 0] = np.where(np.isinf(k), k, k * np.float32(1e3)).astype(np.float32)  # sphere-like k too
-        got = _device(box, ray, rg, km, 2)
+        got = _device(box, ray, rg, km, mode)
         fast = (got & 4) != 0
         sah, exact = (got & 1) != 0, (got & 2) != 0
         assert fast.mean() > 0.5
