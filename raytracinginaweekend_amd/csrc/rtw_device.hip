@@ -1457,7 +1457,10 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 #ifndef RTW_C2_UNROLL
 #define RTW_C2_UNROLL 3
 #endif
-        for (int u = 0; u < (STATS ? 1 : C2 ? RTW_C2_UNROLL : RTW_TRAV_UNROLL); ++u) {
+#ifndef RTW_FB_UNROLL
+#define RTW_FB_UNROLL 1  // the re-trace loop (rare rays): no unrolling, a smaller kernel (suzanne +0.8 %, profiles/r03/v7_code_size_ab.txt)
+#endif
+        for (int u = 0; u < (STATS ? 1 : C2 ? RTW_C2_UNROLL : TM == TM_FALLBACK ? RTW_FB_UNROLL : RTW_TRAV_UNROLL); ++u) {
         // leaf bodies on every step, or (LK_SPHERES, LK_TRIS) on even steps only: a lane reaching a
         // leaf then waits up to one step, and the wave runs a leaf body for twice the lanes half as
         // often.  That pays where leaf steps are a small share (final_scene1 ~0.1 leaf per node
