@@ -546,6 +546,27 @@ __device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i
     f.y2 = d.w;
     return f;
 }
+// LDS mode 2 keeps the records component-major: component k of triangle i at tf[k * RTW_TRI_SOA + i].
+// With a compile-time stride the four reads share one address register (offsets 0, 16, 32, 48 KB in
+// the ds_read_b128 immediate), and a 16-lane group's reads of one component spread over all 16 slots
+// of the 256-B bank row instead of the 4 that 64-B records start on (4-way conflicts: suzanne's 2.8
+// conflict cycles per LDS instruction in round 2).  Worlds of at most RTW_TRI_SOA triangles.
+#ifndef RTW_TRI_SOA
+#define RTW_TRI_SOA 1024
+#endif
+__device__ __forceinline__ TriFast load_tri_soa(const float4* __restrict__ tf, int i) {
+    const float4 a = tf[i], b = tf[RTW_TRI_SOA + i], c = tf[2 * RTW_TRI_SOA + i], d = tf[3 * RTW_TRI_SOA + i];
+    TriFast f;
+    f.p0 = v3(a.x, a.y, a.z);
+    f.n = v3(a.w, b.x, b.y);
+    f.vt1 = v3(b.z, b.w, c.x);
+    f.den1 = c.y;
+    f.vt2 = v3(c.z, c.w, d.x);
+    f.den2 = d.y;
+    f.y1 = d.z;
+    f.y2 = d.w;
+    return f;
+}
 // a barycentric quotient a / den with the record's y = RN(1 / den) (0: den out of range)
 __device__ __forceinline__ float div_tri(float a, float den, float y) {
     float q = mk_corr(a, den, y);
@@ -1487,7 +1508,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             } else if (LK == LK_TRIS || LK == LK_PLAIN || __float_as_int(sph.x) == 1) {  // a plain triangle
                 if (STATS) st.c[ST_T_TRI]++;
                 float t;
-                if (tri_test(load_tri(tri_fast, __float_as_int(sph.y)), T.ray, 0.001f, T.te, t)) take(t, leaf);
+                const int ti = __float_as_int(sph.y);
+                if (tri_test(LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), T.ray, 0.001f, T.te, t))
+                    take(t, leaf);
             } else if (LK >= LK_WRAPPED) {
                 float t;
                 if (leaf_t<STATS, LK == LK_ANY>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) take(t, leaf);
@@ -1620,7 +1643,8 @@ __device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, u
                 const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
                 hit = rect_t_mk(g, r, inv, 0.001f, F32_INF, t);  // SAH rays are Markstein-exact
             } else {
-                hit = tri_test(load_tri(tri_fast, __float_as_int(sph.y)), r, 0.001f, F32_INF, t);
+                const int ti = __float_as_int(sph.y);
+                hit = tri_test(LDS == 2 ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), r, 0.001f, F32_INF, t);
             }
             if (hit) {
                 cnt = t == best ? cnt + 1 : t < best ? 1u : cnt;
@@ -1688,7 +1712,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         for (int i = threadIdx.x; i < 2 * A.rect_count; i += RTW_BLOCK) rects[i] = w.rects[i];
         if (LDS == 2) {
             float4* tris = rects + 2 * A.rect_count;
-            for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[i] = w.tri_fast[i];
+            for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[(i & 3) * RTW_TRI_SOA + (i >> 2)] = w.tri_fast[i];
         }
         if (A.sh_li >= 0) {  // shading tables (launch_render decides whether they fit)
             int4* li = reinterpret_cast<int4*>(smem + A.sh_li);
@@ -3135,7 +3159,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     A.node_count = sah ? g->sah_nodes : g->node_count;
     const size_t scene_bytes =
         (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
-    const size_t tri_bytes = (size_t)g->tri_count * 4 * sizeof(float4);
+    const size_t tri_bytes = (size_t)4 * RTW_TRI_SOA * sizeof(float4);  // mode 2: component-major, fixed stride
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
     const size_t stack16_bytes = stack_bytes / 2;  // mode 2: 16-bit entries
     // a block may take its share of the CU's LDS at the kernel's target occupancy
@@ -3143,7 +3167,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const int blocks_per_cu = std::max(1, (4 * RTW_MIN_WAVES_PER_SIMD * 64) / RTW_BLOCK);
     const size_t cap = std::min({(size_t)RTW_LDS_SCENE_MAX, (size_t)g->lds_max, (size_t)g->lds_cu / blocks_per_cu});
     int mode = 0;
-    if (g->tri_count > 0 && g->leaf_count < 32768 && A.node_count < 32768 && g->node_count < 32768 &&
+    if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 && A.node_count < 32768 && g->node_count < 32768 &&
         scene_bytes + tri_bytes + stack16_bytes <= cap)
         mode = 2;
     else if (scene_bytes + stack_bytes <= cap) mode = 1;
