@@ -1419,6 +1419,13 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // the pushed child's entry t, so that a pop skips children starting beyond te, lost 5 %: the
     // skip loop's divergence costs more than the node steps it saves, profiles/r02/v9_two_child_ab.txt.)
     constexpr bool C2 = TM == TM_SAH && LK == LK_SPHERES;
+#ifndef RTW_C2_INLINE
+#define RTW_C2_INLINE 1
+#endif
+    // the two-children step tests a leaf child's sphere at once: leaves are never pushed or stood on,
+    // so the loop has no leaf steps (final_scene1 +3.0 %, profiles/r03/v9_inline_leaf_ab.txt;
+    // RTW_C2_INLINE=0 builds keep round 2's leaf-then-node step)
+    constexpr bool C2_INLINE = C2 && RTW_C2_INLINE;
     // the SAH node test's k term: D^2 (two operations; every world gained 0.5 %,
     // profiles/r03/v6_delta_d2_ab.txt); RTW_SAH_DQ builds keep round 2's Dq form
 #ifdef RTW_SAH_DQ
@@ -1489,7 +1496,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         // wall rects, ~0.8: -8 %), hence only for worlds without rect, box or wrapped leaves.
         // The two-children step of plain-sphere SAH walks (C2) halves the node steps between leaves:
         // there a leaf body on every step is 3 % faster (profiles/r02/v9_leaf_cadence_ab.txt).
-        if ((STATS || C2 || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
+        if (!C2_INLINE && (STATS || C2 || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
             const int leaf = -1 - T.node;
             const float4 sph = fast[leaf];
             if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
@@ -1534,14 +1541,37 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             const float2 ch = reinterpret_cast<const float2*>(nodes_b)[2 * T.node + 1];
             const int32_t left = __float_as_int(ch.x) >> 2, right = __float_as_int(ch.y);
             const int32_t il = left >= 0 ? left : 0, ir = right >= 0 ? right : 0;
-            const float4 la = nodes_a[il], lb = nodes_b[il], ra = nodes_a[ir], rb = nodes_b[ir];
-            const float2 lk = nkm[il], rk = nkm[ir];
             float el, er;
-            if (STATS) st.c[ST_NODES] += (left >= 0) + (right >= 0);  // the child boxes tested
-            const bool pl = node_pass_cons<SAH_DQ>(la, lb, lk, T.ray, rp, 0.001f, T.te, el) || left < 0;
-            const bool pr = node_pass_cons<SAH_DQ>(ra, rb, rk, T.ray, rp, 0.001f, T.te, er) || right < 0;
-            if (left < 0) el = -F32_INF;
-            if (right < 0) er = -F32_INF;
+            bool pl, pr;
+            if (C2_INLINE) {
+                // leaf children: their sphere now (never pushed or visited); internal ones: the box
+                pl = pr = false;
+                el = er = F32_INF;
+                if (left < 0) {
+                    if (STATS) st.c[ST_T_SPHERE]++;
+                    float t;
+                    if (sphere_t(fast[-1 - left], T.ray, 0.001f, T.te, t)) take(t, -1 - left);
+                } else {
+                    if (STATS) st.c[ST_NODES]++;
+                    pl = node_pass_cons<SAH_DQ>(nodes_a[left], nodes_b[left], nkm[left], T.ray, rp, 0.001f, T.te, el);
+                }
+                if (right < 0) {
+                    if (STATS) st.c[ST_T_SPHERE]++;
+                    float t;
+                    if (sphere_t(fast[-1 - right], T.ray, 0.001f, T.te, t)) take(t, -1 - right);
+                } else {
+                    if (STATS) st.c[ST_NODES]++;
+                    pr = node_pass_cons<SAH_DQ>(nodes_a[right], nodes_b[right], nkm[right], T.ray, rp, 0.001f, T.te, er);
+                }
+            } else {
+                const float4 la = nodes_a[il], lb = nodes_b[il], ra = nodes_a[ir], rb = nodes_b[ir];
+                const float2 lk = nkm[il], rk = nkm[ir];
+                if (STATS) st.c[ST_NODES] += (left >= 0) + (right >= 0);  // the child boxes tested
+                pl = node_pass_cons<SAH_DQ>(la, lb, lk, T.ray, rp, 0.001f, T.te, el) || left < 0;
+                pr = node_pass_cons<SAH_DQ>(ra, rb, rk, T.ray, rp, 0.001f, T.te, er) || right < 0;
+                if (left < 0) el = -F32_INF;
+                if (right < 0) er = -F32_INF;
+            }
             if (pl && pr) {
                 const bool lf = el <= er;
                 stack[(T.sp++) * RTW_BLOCK] = (StackEntry)(lf ? right : left);
