@@ -1441,6 +1441,34 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
     const RayPre rp{T.inv, (T.fast & 8) != 0};
+    // one leaf's test at the current t range (hittable.rs:436-437: a leaf is never box-tested)
+    auto test_leaf = [&](int leaf) {
+        const float4 sph = fast[leaf];
+        if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
+            if (STATS) st.c[ST_T_SPHERE]++;
+            float t;
+            if (sphere_t(sph, T.ray, 0.001f, T.te, t)) take(t, leaf);
+        } else if (LK >= LK_PLAIN && __float_as_int(sph.x) == 2) {  // a plain rect
+            if (STATS) st.c[ST_T_RECT]++;
+            const int ri = __float_as_int(sph.y);
+            const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
+            const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
+            float t;
+            V3 pos;
+            if (FAST_ONLY ? rect_t_mk(g, T.ray, rp.inv, 0.001f, T.te, t) : rect_t(g, T.ray, 0.001f, T.te, t, pos))
+                take(t, leaf);
+        } else if (LK == LK_TRIS || LK == LK_PLAIN || __float_as_int(sph.x) == 1) {  // a plain triangle
+            if (STATS) st.c[ST_T_TRI]++;
+            float t;
+            const int ti = __float_as_int(sph.y);
+            if (tri_test(LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), T.ray, 0.001f, T.te, t))
+                take(t, leaf);
+        } else if (LK >= LK_WRAPPED) {
+            float t;
+            if (leaf_t<STATS, LK == LK_ANY>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) take(t, leaf);
+        }
+    };
+
     // execution counters, summed over lanes at the end: wave-level events are counted by the
     // first active lane of the wave (or of the branch) only
     uint32_t db[DB_SHADE_CALLS] = {};
@@ -1497,31 +1525,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         // The two-children step of plain-sphere SAH walks (C2) halves the node steps between leaves:
         // there a leaf body on every step is 3 % faster (profiles/r02/v9_leaf_cadence_ab.txt).
         if (!C2_INLINE && (STATS || C2 || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
-            const int leaf = -1 - T.node;
-            const float4 sph = fast[leaf];
-            if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
-                if (STATS) st.c[ST_T_SPHERE]++;
-                float t;
-                if (sphere_t(sph, T.ray, 0.001f, T.te, t)) take(t, leaf);
-            } else if (LK >= LK_PLAIN && __float_as_int(sph.x) == 2) {  // a plain rect
-                if (STATS) st.c[ST_T_RECT]++;
-                const int ri = __float_as_int(sph.y);
-                const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
-                const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
-                float t;
-                V3 pos;
-                if (FAST_ONLY ? rect_t_mk(g, T.ray, rp.inv, 0.001f, T.te, t) : rect_t(g, T.ray, 0.001f, T.te, t, pos))
-                    take(t, leaf);
-            } else if (LK == LK_TRIS || LK == LK_PLAIN || __float_as_int(sph.x) == 1) {  // a plain triangle
-                if (STATS) st.c[ST_T_TRI]++;
-                float t;
-                const int ti = __float_as_int(sph.y);
-                if (tri_test(LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), T.ray, 0.001f, T.te, t))
-                    take(t, leaf);
-            } else if (LK >= LK_WRAPPED) {
-                float t;
-                if (leaf_t<STATS, LK == LK_ANY>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) take(t, leaf);
-            }
+            test_leaf(-1 - T.node);
             pop();
         }
         if (STATS) {
@@ -1600,7 +1604,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 // SAH walk: a leaf child first (its hit shrinks te before the sibling subtree; suzanne
                 // +2.2 %, profiles/r02/v9_two_child_ab.txt)
                 if (TM == TM_SAH && (left < 0) != (right < 0)) fwd = left < 0;
-                // hit_index_list order: near subtree, then far
+                // hit_index_list order: near subtree, then far (triangle / rect worlds keep leaf steps:
+                // testing leaf children inside this step cost suzanne 17 %, profiles/r03/v10_unroll_c1_ab.txt)
                 stack[(T.sp++) * RTW_BLOCK] = (StackEntry)(fwd ? right : left);
                 T.node = fwd ? left : right;
             } else if (T.sp == 0) {
