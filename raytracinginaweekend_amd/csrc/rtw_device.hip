@@ -39,7 +39,8 @@
 #define RTW_MIN_WAVES_PER_SIMD 4
 #endif
 #ifndef RTW_WAVE_BATCH
-#define RTW_WAVE_BATCH 64  // work items a wave reserves per global atomic (upper bound)
+#define RTW_WAVE_BATCH 128  // work items a wave reserves per global atomic (upper bound; 64: final_scene1
+                            // -0.9 %, earth_motion -0.9 %, profiles/r03/v12_queue_batch_ab.txt)
 #endif
 #ifndef RTW_WAVE_BATCH_BIG
 #define RTW_WAVE_BATCH_BIG 1024  // the same past the first items of a launch (the costly tiles in cost order)
