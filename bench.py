@@ -197,15 +197,36 @@ def cpu_baseline(args) -> dict:
     }
 
 
+def count_gpus() -> int:
+    """GPUs this process could use, counted without any HIP call (the parent of the rank processes
+    must not initialise the GPU): the KFD topology's GPU nodes (simd_count > 0), narrowed by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set."""
+    import glob
+
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            for line in open(f):
+                k, _, v = line.partition(" ")
+                if k == "simd_count" and int(v) > 0:
+                    n += 1
+                    break
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(args) -> int:
     """--gpus N > 1 without a launcher: one rank process per GPU, started before this process
-    touches the GPU (counting devices does not initialise it); rank 0 prints the line."""
+    touches the GPU (count_gpus makes no HIP call); rank 0 prints the line."""
     import socket
     import subprocess
 
-    import torch
-
-    n = torch.cuda.device_count()
+    n = count_gpus()
     if n < args.gpus:
         print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {n}", file=sys.stderr)
         return 3

@@ -227,6 +227,31 @@ static int rtw_wrap_box(const rtw_leaf* L, float t0, float t1, const float llo[3
     return 1;
 }
 
+/* The interval every ray's time lies in (camera.rs:186-190): start in [time0, time1] (gen_range, or
+ * time0 when equal) plus dot(shutter_pace, (px, py)) at the jittered pixel coordinates px, py in [0, 2]
+ * (px = x / (W - 1) <= 1 plus a jitter below 1 / (W - 1) <= 1).  With a non-zero pace the device's f32
+ * products and sums round (at most 4u of the magnitudes involved), so the bounds move out by 2^-20 of
+ * them; rounded outward to f32.  0 if not finite. */
+static int rtw_ray_time_range(const rtw_camera* c, float* lo, float* hi) {
+    const double a = c->time0 < c->time1 ? c->time0 : c->time1, b = c->time0 < c->time1 ? c->time1 : c->time0;
+    const double p0 = c->shutter_pace[0], p1 = c->shutter_pace[1];
+    if (!(fabs(a) < 1e300 && fabs(b) < 1e300 && fabs(p0) < 1e300 && fabs(p1) < 1e300)) return 0;
+    if (p0 == 0.0 && p1 == 0.0) {
+        *lo = (float)a;
+        *hi = (float)b;
+        return 1;
+    }
+    const double U = 2.0 + 0x1p-16;
+    const double M = fmax(fabs(a), fabs(b)) + U * (fabs(p0) + fabs(p1));
+    const double l = a + U * (fmin(0.0, p0) + fmin(0.0, p1)) - M * 0x1p-20;
+    const double h = b + U * (fmax(0.0, p0) + fmax(0.0, p1)) + M * 0x1p-20;
+    *lo = (float)l;
+    *hi = (float)h;
+    if ((double)*lo > l) *lo = nextafterf(*lo, -INFINITY);
+    if ((double)*hi < h) *hi = nextafterf(*hi, INFINITY);
+    return *lo > -INFINITY && *hi < INFINITY;
+}
+
 /* One leaf's constants and the box its accepted hit points lie within delta of.  wrapped = 0: plain
  * leaves only (the reference tree); 1: Transformation / Animation leaves too, with their true world
  * boxes (trees built over those).  Volumes: never.  0 if not cullable; *never = 1 if it can never
@@ -255,7 +280,9 @@ static int rtw_cull_leaf(const rtw_world* w, const rtw_leaf* L, int wrapped, flo
         for (int i = 0; i < 3; ++i) { lo[i] = llo[i]; hi[i] = lhi[i]; }
         return 1;
     }
-    const float t0 = w->camera.time0, t1 = w->camera.time1;
+    /* Animation offsets sweep over every ray time, the rolling shutter's included */
+    float t0, t1;
+    if (!rtw_ray_time_range(&w->camera, &t0, &t1)) return 0;
     if (!rtw_wrap_box(L, t0, t1, llo, lhi, lo, hi)) return 0;
     const float T = rtw_maxr(__builtin_fabsf(t0), __builtin_fabsf(t1));
     float A = 0.0f, off = 0.0f, vel = 0.0f;

@@ -321,13 +321,13 @@ def lib() -> C.CDLL:
             fn.argtypes = args
         if L.rtw_version() != ABI_VERSION:
             msg = f"{LIB_PATH} has ABI version {L.rtw_version()}, this package needs {ABI_VERSION}"
-            if not os.environ.get("RTW_LIBRARY"):
-                raise ImportError(msg + ": rebuild it")
-            # experiment builds (RTW_LIBRARY) may predate an ABI change: say so instead of rendering
-            # with a misread rtw_render_params
+            # a mismatched library would read rtw_render_params wrongly: refuse it, unless an A/B run
+            # of an older experiment build (RTW_LIBRARY) opts in explicitly
+            if not (os.environ.get("RTW_LIBRARY") and os.environ.get("RTW_ALLOW_ABI_MISMATCH") == "1"):
+                raise ImportError(msg + ": rebuild it (A/B runs of older builds: RTW_ALLOW_ABI_MISMATCH=1)")
             import warnings
 
-            warnings.warn(msg + " (RTW_LIBRARY override): thread_count and later fields are not honoured")
+            warnings.warn(msg + " (RTW_ALLOW_ABI_MISMATCH=1): thread_count and later fields are not honoured")
         _lib = L
     return _lib
 

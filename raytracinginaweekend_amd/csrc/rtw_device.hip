@@ -1159,6 +1159,29 @@ __device__ __forceinline__ Ray camera_ray(const rtw_camera& c, rtw_xoro& rng, fl
 // shading: one bounce of ray_color (rendering.rs:19-71), out of line so that its temporaries
 // and hoisted invariants never pressure the traversal loop's registers
 // ---------------------------------------------------------------------------------------------
+// Experiment builds only (make variant DEFS=-DRTW_PHASE_TIMING): per-wave wall cycles of the main
+// loop's phases, summed over waves into rtw_phase_cycles (read by rtw_debug_phase_cycles).
+// The phase is a property of the wave: it lives in LDS (per wave: 8 sums, the last stamp, the current
+// phase), and the first active lane switches it, so that a switch inside divergent code (the shading
+// lanes' samplers) charges the wave's cycles to the right phase.  Phases: 1 refill (work items),
+// 2 traversal setup, 3 traversal (walk, drain, proof, re-trace), 4 shading, 5 sample start (stream
+// setup, jitter, camera ray with its UnitDisc), 6 shading's samplers (UnitSphere / UnitBall /
+// gen_bool / light direction), 7 colour store and cost bookkeeping.
+#ifdef RTW_PHASE_TIMING
+__device__ unsigned long long rtw_phase_cycles[8];
+__device__ __forceinline__ unsigned long long* pt_slot() {
+    __shared__ unsigned long long s[(RTW_BLOCK / 64) * 10];
+    return s + (threadIdx.x >> 6) * 10;
+}
+#define RTW_PT_DECL do { unsigned long long* s_ = pt_slot(); if ((threadIdx.x & 63) == 0) { for (int k_ = 0; k_ < 8; ++k_) s_[k_] = 0; s_[8] = clock64(); s_[9] = 0; } } while (0);
+#define RTW_PT(k) do { if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) { unsigned long long* s_ = pt_slot(); const unsigned long long now_ = clock64(); s_[s_[9]] += now_ - s_[8]; s_[8] = now_; s_[9] = (k); } } while (0)
+#define RTW_PT_FLUSH do { RTW_PT(0); if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&rtw_phase_cycles[k_], pt_slot()[k_]); } while (0)
+#else
+#define RTW_PT_DECL
+#define RTW_PT(k) do { } while (0)
+#define RTW_PT_FLUSH do { } while (0)
+#endif
+
 struct Path {  // per-path state crossing the call by value (registers)
     Ray ray;
     V3 att, acc;
@@ -1212,7 +1235,9 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                     V3 fz = v3(0.0f, 0.0f, 0.0f);
                     if (fuzz > 0.0f) {
                         float b[3];
+                        RTW_PT(6);
                         rtw_unit_ball(&rng, b);
+                        RTW_PT(4);
                         fz = mul(v3(b[0], b[1], b[2]), fuzz);
                     }
                     const V3 dir = add(reflect(ray.d, h.n), fz);
@@ -1247,6 +1272,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                 // sample_final_scattering_distribution (rendering.rs:73-92): the mixture draws its
                 // bool before either generator.
                 bool light_dir = false;
+                RTW_PT(6);
                 if (cosine) {
                     if (w.has_light) light_dir = rtw_gen_bool_half(&rng);
                     need_sphere = !light_dir;
@@ -1269,6 +1295,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                         sdir = sv;
                     }
                 }
+                RTW_PT(4);
                 const V3 tc = (tex >= 0) ? texture_sample<STATS, TX>(w, tex, h, st, S) : v3(0.0f, 0.0f, 0.0f);
                 const V3 emitted = (mkind == RTW_MAT_DIFFUSE_LIGHT) ? tc : v3(0.0f, 0.0f, 0.0f);
                 const V3 albedo = (mkind == RTW_MAT_DIELECTRIC) ? v3(1.0f, 1.0f, 1.0f) : tc;
@@ -1329,18 +1356,6 @@ enum { TM_REF = 0, TM_SAH = 1, TM_FALLBACK = 2 };
 #define RTW_TF_SAH 16  // the ray is traced on the SAH tree; te = the closest t's successor
 #define RTW_TF_TIE 32  // another leaf reported exactly the closest t
 
-// Experiment builds only (make variant DEFS=-DRTW_PHASE_TIMING): per-wave wall cycles of the main
-// loop's phases, summed over waves into rtw_phase_cycles (read by rtw_debug_phase_cycles).
-#ifdef RTW_PHASE_TIMING
-__device__ unsigned long long rtw_phase_cycles[8];
-#define RTW_PT_DECL uint64_t pt_last = clock64(); uint64_t pt_acc[8] = {}; int pt_cur = 0;
-#define RTW_PT(k) do { const uint64_t now_ = clock64(); pt_acc[pt_cur] += now_ - pt_last; pt_last = now_; pt_cur = (k); } while (0)
-#define RTW_PT_FLUSH do { RTW_PT(0); if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&rtw_phase_cycles[k_], (unsigned long long)pt_acc[k_]); } while (0)
-#else
-#define RTW_PT_DECL
-#define RTW_PT(k) do { } while (0)
-#define RTW_PT_FLUSH do { } while (0)
-#endif
 
 // Traversal state of one lane (by value, in registers, across the out-of-line call).
 struct Trav {
@@ -1644,7 +1659,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 // tree).  Rays of `todo` only (SAH rays: RTW_TF_SAH).  `audit` (tests only, RTW_COOP_AUDIT=1) takes
 // the DFS-last tied leaf instead: wrong images, which shows that the resolution decides them.
 template <int LDS, int LK>
-__device__ __noinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, unsigned long long todo, int32_t n_nodes,
+__device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, unsigned long long todo, int32_t n_nodes,
                                         int32_t n_leaves, int32_t n_rects, bool audit) {
     const DWorld& w = *wp;
     constexpr bool LDS_SCENE = LDS >= 1;
@@ -1793,7 +1808,9 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     uint64_t c_mark = STATS ? clock64() : 0;  // execution-time split (counting variant only)
 
     // rendering.rs:174-176: jitter (x then y), then Camera::ray
-    auto start_sample = [&]() {
+    auto start_sample = [&](int back) {
+        (void)back;
+        RTW_PT(5);
         T.rng = rtw_sample_stream(A.seed_key, pix, sample);
         const float jx = rtw_uniform_sample(&A.ux, &T.rng);
         const float jy = rtw_uniform_sample(&A.uy, &T.rng);
@@ -1803,6 +1820,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         acc = v3(0.0f, 0.0f, 0.0f);
         depth = A.max_depth;
         fresh = true;
+        RTW_PT(back);
     };
 
     int32_t trace_min = A.trace_min;  // this wave's dynamic-fetch threshold (tuned below)
@@ -1960,7 +1978,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         fy = (float)py * A.sy;
                         sample = big ? A.s_begin + ck * A.chunk : A.s_split + ck;
                         sample_end = big ? min(sample + A.chunk, A.s_split) : sample + 1;
-                        start_sample();
+                        start_sample(1);
                         T.phase = PH_TRACE;
                     }
                 }
@@ -2016,6 +2034,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
                                                        A.leaf_count, A.rect_count, A.tri_count, stack_off,
                                                        STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
+            // the rays coop_trace takes (one call site, inlined: as an out-of-line call taking and
+            // returning Trav by value it cost 304 B of scratch per lane, saved and restored around
+            // every call -- suzanne's and cornell_cube's extra write traffic): the drain's last rays
+            unsigned long long coop = 0;
             if (dry_coop) {
                 const unsigned long long tm = __ballot(T.phase == PH_TRACE);
 #ifdef RTW_WAVE_TIMING
@@ -2024,9 +2046,14 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 wx_tsah += wx_tc - wx_t0;  // the walk part
                 wx_t0 = wx_tc;
 #endif
-                if (tm != 0 && (uint32_t)__popcll(tm) <= (uint32_t)A.coop_max)
-                    T = coop_trace<LDS, LK>(A.wdev, T, tm, A.node_count, A.leaf_count, A.rect_count, A.coop_ties == 2);
+                if (tm != 0 && (uint32_t)__popcll(tm) <= (uint32_t)A.coop_max) coop = tm;
             }
+            // ... and the walk's tied rays: coop_trace finds every tied leaf and keeps the reference's
+            // (its DFS-first); a drained ray is traced once and leaves with its own ties resolved
+            if (!STATS && LK <= LK_PLAIN && A.coop_ties)
+                coop |= __ballot(T.phase == PH_SHADE && (T.fast & (RTW_TF_SAH | RTW_TF_TIE)) == (RTW_TF_SAH | RTW_TF_TIE));
+            if (!STATS && LK <= LK_PLAIN && coop)
+                T = coop_trace<LDS, LK>(A.wdev, T, coop, A.node_count, A.leaf_count, A.rect_count, A.coop_ties == 2);
 #ifdef RTW_WAVE_TIMING
             const uint64_t wx_t1 = wall_clock64();
             if (qfail >= RTW_QUEUES) wx_tcoop += wx_t1 - wx_t0;
@@ -2044,12 +2071,6 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             // and hit_cond is monotone under box inclusion and in te, so L's parent box passing
             // hit_cond with te = succ(t) proves it.  A miss is a miss for the reference too.
             // Otherwise the ray is traced again on the reference tree.
-            // walk ties: coop_trace finds every tied leaf and keeps the reference's (its DFS-first)
-            if (!STATS && LK <= LK_PLAIN && A.coop_ties) {
-                const unsigned long long tl =
-                    __ballot(T.phase == PH_SHADE && (T.fast & (RTW_TF_SAH | RTW_TF_TIE)) == (RTW_TF_SAH | RTW_TF_TIE));
-                if (tl) T = coop_trace<LDS, LK>(A.wdev, T, tl, A.node_count, A.leaf_count, A.rect_count, A.coop_ties == 2);
-            }
             if (T.phase == PH_SHADE && (T.fast & RTW_TF_SAH)) {
                 bool ok = (T.fast & RTW_TF_TIE) == 0;
 #ifdef RTW_SAH_AUDIT_NO_TIE  // audit builds only: shows that the tie test decides images
@@ -2136,6 +2157,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             if (STATS) st.c[ST_TEXEL] += so.texels;
             T.phase = PH_TRACE;
             if (so.done) {
+                RTW_PT(7);
                 float* o = A.colors + ((uint64_t)(sample - A.s_begin) * A.total + slot) * 3;
                 o[0] = so.color.x;
                 o[1] = so.color.y;
@@ -2154,7 +2176,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 #endif
                 ++sample;
                 if (sample >= sample_end) T.phase = PH_PIXEL;
-                else start_sample();
+                else start_sample(7);
             } else {
                 fresh = true;  // the scattered ray continues the path
             }
@@ -2577,11 +2599,15 @@ int check_world(const rtw_world* w, int* depth_out) {
         if (big(w->spheres[i].center, 4)) return bad("sphere beyond 2^30");
     for (int i = 0; i < w->rect_count; ++i)
         if (big(&w->rects[i].dist, 1)) return bad("rect beyond 2^30");
+    // an Animation offset is velocity x ray time, the rolling shutter's pace included (rtw_ray_time_range)
+    float rt0 = 0.0f, rt1 = 0.0f;
+    const float tmax = rtw_ray_time_range(&w->camera, &rt0, &rt1) ? std::max(std::fabs(rt0), std::fabs(rt1))
+                                                                   : std::numeric_limits<float>::infinity();
     for (int i = 0; i < w->leaf_count; ++i) {
         const rtw_leaf& L = w->leaves[i];
         float vt[3];
         for (int k = 0; k < 3; ++k)
-            vt[k] = L.velocity[k] * std::max(std::fabs(w->camera.time0), std::fabs(w->camera.time1));
+            vt[k] = (L.flags & RTW_LEAF_ANIMATION) && L.velocity[k] != 0.0f ? L.velocity[k] * tmax : 0.0f;
         if (big(L.offset, 3) || big(vt, 3)) return bad("leaf transform beyond 2^30");
     }
     if (big(w->camera.position, 3)) return bad("camera beyond 2^30");
@@ -3201,7 +3227,10 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     // a block may take its share of the CU's LDS at the kernel's target occupancy
     // (RTW_MIN_WAVES_PER_SIMD waves on each of 4 SIMDs)
     const int blocks_per_cu = std::max(1, (4 * RTW_MIN_WAVES_PER_SIMD * 64) / RTW_BLOCK);
-    const size_t cap = std::min({(size_t)RTW_LDS_SCENE_MAX, (size_t)g->lds_max, (size_t)g->lds_cu / blocks_per_cu});
+    size_t cap = std::min({(size_t)RTW_LDS_SCENE_MAX, (size_t)g->lds_max, (size_t)g->lds_cu / blocks_per_cu});
+#ifdef RTW_PHASE_TIMING
+    cap -= (RTW_BLOCK / 64) * 10 * sizeof(unsigned long long);  // the per-wave phase sums (pt_slot)
+#endif
     int mode = 0;
     if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 && A.node_count < 32768 && g->node_count < 32768 &&
         scene_bytes + tri_bytes + stack16_bytes <= cap)
@@ -3684,6 +3713,22 @@ extern "C" RTW_API int rtw_encode_rgb8_device(const float* d_image, int64_t pixe
     return RTW_OK;
 }
 
+namespace {
+// device buffers of the self-check entry points below, freed on every return path
+struct DevBufs {
+    std::vector<void*> p;
+    ~DevBufs() {
+        for (void* q : p) (void)hipFree(q);
+    }
+    template <class T>
+    hipError_t alloc(T** x, size_t bytes) {
+        const hipError_t e = hipMalloc((void**)x, bytes);
+        if (e == hipSuccess) p.push_back((void*)*x);
+        return e;
+    }
+};
+}  // namespace
+
 extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, const float* ray, const float* range,
                                                  const float* km, int32_t mk_world, int64_t n, int32_t* out) {
     if (!box || !ray || !range || !km || !out || n < 0) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
@@ -3693,11 +3738,12 @@ extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, c
     if (n == 0) return RTW_OK;
     float *db = nullptr, *dr = nullptr, *dg = nullptr, *dk = nullptr;
     int32_t* dout = nullptr;
-    HIP_TRY(hipMalloc(&db, (size_t)n * 6 * sizeof(float)));
-    HIP_TRY(hipMalloc(&dr, (size_t)n * 6 * sizeof(float)));
-    HIP_TRY(hipMalloc(&dg, (size_t)n * 2 * sizeof(float)));
-    HIP_TRY(hipMalloc(&dk, (size_t)n * 2 * sizeof(float)));
-    HIP_TRY(hipMalloc(&dout, (size_t)n * sizeof(int32_t)));
+    DevBufs bufs;
+    HIP_TRY(bufs.alloc(&db, (size_t)n * 6 * sizeof(float)));
+    HIP_TRY(bufs.alloc(&dr, (size_t)n * 6 * sizeof(float)));
+    HIP_TRY(bufs.alloc(&dg, (size_t)n * 2 * sizeof(float)));
+    HIP_TRY(bufs.alloc(&dk, (size_t)n * 2 * sizeof(float)));
+    HIP_TRY(bufs.alloc(&dout, (size_t)n * sizeof(int32_t)));
     HIP_TRY(hipMemcpy(db, box, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dr, ray, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dg, range, (size_t)n * 2 * sizeof(float), hipMemcpyHostToDevice));
@@ -3706,11 +3752,6 @@ extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, c
                        n, dout);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpy(out, dout, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
-    (void)hipFree(db);
-    (void)hipFree(dr);
-    (void)hipFree(dg);
-    (void)hipFree(dk);
-    (void)hipFree(dout);
     return RTW_OK;
 }
 
@@ -3721,14 +3762,14 @@ extern "C" RTW_API int rtw_device_check_division(int device, int test, uint64_t 
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device");
     HIP_TRY(hipSetDevice(device));
     unsigned long long* d = nullptr;
-    HIP_TRY(hipMalloc(&d, 2 * sizeof(unsigned long long)));
+    DevBufs bufs;
+    HIP_TRY(bufs.alloc(&d, 2 * sizeof(unsigned long long)));
     const unsigned long long init[2] = {0ull, ~0ull};
     HIP_TRY(hipMemcpy(d, init, sizeof(init), hipMemcpyHostToDevice));
     hipLaunchKernelGGL(check_division_kernel, dim3(8192), dim3(256), 0, 0, test, base, n, seed, d);
     HIP_TRY(hipGetLastError());
     unsigned long long res[2];
     HIP_TRY(hipMemcpy(res, d, sizeof(res), hipMemcpyDeviceToHost));
-    (void)hipFree(d);
     *mismatches = res[0];
     *first = res[1];
     return RTW_OK;
@@ -3742,14 +3783,13 @@ extern "C" RTW_API int rtw_device_eval_checker(int device, const float* xyz, int
     if (n == 0) return RTW_OK;
     float* dx = nullptr;
     int32_t* dout = nullptr;
-    HIP_TRY(hipMalloc(&dx, (size_t)n * 3 * sizeof(float)));
-    HIP_TRY(hipMalloc(&dout, (size_t)n * sizeof(int32_t)));
+    DevBufs bufs;
+    HIP_TRY(bufs.alloc(&dx, (size_t)n * 3 * sizeof(float)));
+    HIP_TRY(bufs.alloc(&dout, (size_t)n * sizeof(int32_t)));
     HIP_TRY(hipMemcpy(dx, xyz, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice));
     hipLaunchKernelGGL(eval_checker_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, n, dout);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpy(out, dout, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
-    (void)hipFree(dx);
-    (void)hipFree(dout);
     return RTW_OK;
 }
 
@@ -3761,16 +3801,14 @@ extern "C" RTW_API int rtw_device_eval_scalar(int device, int fn, const float* a
     if (n == 0) return RTW_OK;
     float *da = nullptr, *db = nullptr, *dout = nullptr;
     const size_t bytes = (size_t)n * sizeof(float);
-    HIP_TRY(hipMalloc(&da, bytes));
-    HIP_TRY(hipMalloc(&db, bytes));
-    HIP_TRY(hipMalloc(&dout, bytes));
+    DevBufs bufs;
+    HIP_TRY(bufs.alloc(&da, bytes));
+    HIP_TRY(bufs.alloc(&db, bytes));
+    HIP_TRY(bufs.alloc(&dout, bytes));
     HIP_TRY(hipMemcpy(da, a, bytes, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(db, b ? b : a, bytes, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(eval_scalar_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, fn, da, db, n, dout);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost));
-    (void)hipFree(da);
-    (void)hipFree(db);
-    (void)hipFree(dout);
     return RTW_OK;
 }

@@ -2,14 +2,16 @@
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Rank r renders the
 tiles t with t % N == r of the frame into a compact tile buffer (RTW_LAYOUT_TILES); the buffers
-(padded to rank 0's size, rtw_partition_floats) are all-gathered and rank 0 scatters them into
-the image (rtw_untile_device).  Because the RNG stream is keyed by (seed, pixel, sample), the
+(padded to rank 0's size, rtw_partition_floats) are gathered onto rank 0 (one collective: RCCL's
+gather is a group of point-to-point sends to rank 0 over xGMI, W*H*12/N bytes per peer) and rank 0
+scatters them into the image (rtw_untile_device).  Only rank 0 holds the gather buffer and the image.  Because the RNG stream is keyed by (seed, pixel, sample), the
 image is bit-identical for every N.  PyTorch is plumbing here: device memory, the stream and the
 collective; the render itself is librtw.so's kernel.
 
 TileExchange holds the partition arithmetic and the gather/untile step for both device tensors
 (RCCL + the untile kernel) and host tensors (gloo + untile_host, the CPU mirror used by the
-world-size-2 tests).
+world-size-2 and -3 tests).  Reference: rendering.rs:222-252 (the reference merges per-thread planes
+in one process; here the ranks own disjoint pixels, so the merge is a placement).
 """
 from __future__ import annotations
 
@@ -83,14 +85,17 @@ class TileExchange:
     def pixels_this_rank(self) -> int:
         return int((tile_slots(self.spec.size, self.spec.tile, (self.rank, self.world_size)) >= 0).sum())
 
-    def gather(self, tiles, gathered) -> None:
-        """All-gather the padded tile buffers (RCCL for device tensors, gloo for host ones)."""
+    def gather(self, tiles, gathered=None) -> None:
+        """Gather the padded tile buffers onto rank 0 (RCCL for device tensors, gloo for host ones):
+        rank r's buffer lands at gathered[r * stride : (r + 1) * stride] of rank 0's `gathered`;
+        other ranks pass None (they send only)."""
         import torch.distributed as dist
 
-        if tiles.is_cuda:
-            dist.all_gather_into_tensor(gathered, tiles)
+        if self.rank == 0:
+            parts = list(gathered.view(self.world_size, -1).unbind(0))
+            dist.gather(tiles, parts, dst=0)
         else:
-            dist.all_gather(list(gathered.view(self.world_size, -1).unbind(0)), tiles)
+            dist.gather(tiles, None, dst=0)
 
     def untile(self, gathered, image, stream_ptr: int | None = None) -> None:
         """Rank 0: scatter the gathered buffers into the (W*H*3) image."""
@@ -120,7 +125,8 @@ class FrameRenderer:
         self.image = torch.zeros(npix * 3, dtype=torch.float32, device=self.dev)
         if world_size > 1:
             self.tiles = torch.zeros(self.stride, dtype=torch.float32, device=self.dev)
-            self.gathered = torch.zeros(self.stride * world_size, dtype=torch.float32, device=self.dev)
+            self.gathered = (torch.zeros(self.stride * world_size, dtype=torch.float32, device=self.dev)
+                             if rank == 0 else None)
 
     def stream_ptr(self) -> int:
         return self.torch.cuda.current_stream(self.dev).cuda_stream
@@ -131,7 +137,7 @@ class FrameRenderer:
         self.dworld.render_into(self.params, out.data_ptr(), self.stream_ptr())
 
     def exchange(self) -> None:
-        """One RCCL all-gather of the tile buffers + the untile on rank 0."""
+        """One RCCL gather of the tile buffers onto rank 0 + the untile there."""
         if self.world_size == 1:
             return
         self.xchg.gather(self.tiles, self.gathered)

@@ -1,5 +1,5 @@
 """The multi-GPU data path on the CPU: world-size-2 (and 3) gloo process groups run
-TileExchange -- the same partition arithmetic, padded all-gather and untile as the RCCL path,
+TileExchange -- the same partition arithmetic, padded gather onto rank 0 and untile as the RCCL path,
 with host tensors -- over partition buffers the oracle renders, and rank 0 must reassemble the
 single-process oracle frame bit for bit (the image is independent of N)."""
 import os
@@ -39,7 +39,7 @@ def _worker(rank, world_size, port, out_path, scene, size, spp):
         p = R.render_params(spec.size, spp, 50, seed=99, tile=spec.tile, part=(rank, world_size))
         part_img = O.render(world, p, O.RNG_CTR, 2)
         tiles = torch.from_numpy(pack_tiles(part_img, spec.size, spec.tile, (rank, world_size), x.stride))
-        gathered = torch.zeros(x.stride * world_size, dtype=torch.float32)
+        gathered = torch.zeros(x.stride * world_size, dtype=torch.float32) if rank == 0 else None
         x.gather(tiles, gathered)
         if rank == 0:
             image = torch.zeros(spec.size.width * spec.size.height * 3, dtype=torch.float32)

@@ -47,6 +47,20 @@ def test_full_frame_sampled_tiles_bit_exact(worlds, name, w, h, spp, stride, k):
     assert_bit_identical(gpu[m], ref[m], f"{name} {w}x{h}x{spp}, tiles t % {stride} == {k}")
 
 
+@pytest.mark.parametrize("threads", [1, 16])
+def test_config_c1_every_pixel_bit_exact(worlds, threads):
+    """BASELINE configs[0] (C1): final_scene1 at 400x225x64, max_depth 50 (demo_worlds.rs:395-463 at
+    the explicit size main.rs:38-41 takes), the whole frame through rtw_render and compared with the
+    oracle on EVERY pixel; thread_count 1 and 16 (main.rs:19's available_parallelism on the GPU box:
+    the image is the merge_planes of 16 sample planes, rendering.rs:222-252)."""
+    world = worlds("final_scene1")
+    size = R.Size2i(400, 225)
+    gpu = R.render(size, threads, 64, 50, world, seed=0x5EED)
+    ref = O.render(world, R.render_params(size, 64, 50, seed=0x5EED, thread_count=threads), O.RNG_CTR, threads=16)
+    assert gpu.shape == ref.shape == (400 * 225, 3)
+    assert_bit_identical(gpu, ref, f"C1 final_scene1 400x225x64, thread_count {threads}")
+
+
 def test_full_frame_multi_launch_sampled_tiles(worlds, monkeypatch):
     """The same at 1080p with a colour buffer of ~25 samples per launch: three launches carrying the
     running sum, and the thread_count planes crossing launch boundaries."""

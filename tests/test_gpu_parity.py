@@ -227,6 +227,41 @@ def test_sah_wrapped_ties_and_grazing_hits(monkeypatch):
     assert_bit_identical(sah, R.render(big, 1, 4, 50, world, seed=37), "wrapped tie world, SAH vs reference tree")
 
 
+def _rolling_shutter_world(pace):
+    """Fast-moving spheres under motion blur with a rolling shutter: camera.rs:190 adds
+    dot(shutter_pace, (px, py)) to each ray's start time, so ray times leave [time0, time1]
+    (shutter_pace is a pub field of the reference's Camera, set here the way a Rust caller would)."""
+    wb = R.WorldBuilder()
+    mats = [wb.material_lambert_solid((0.8, 0.2, 0.2)), wb.material_metal_solid((0.7, 0.7, 0.7), 0.0),
+            wb.material_dielectric(1.5), wb.material_lambert_solid((0.2, 0.3, 0.9))]
+    g = wb.new_group()
+    g.add(wb.new_obj_sphere(100.0, mats[0]).translate((0.0, -100.0, 0.0)))
+    for k in range(9):
+        v = ((k % 3 - 1) * 1.5, 0.8 + 0.4 * (k % 2), (k // 3 - 1) * 1.2)
+        g.add(wb.new_obj_sphere(0.22, mats[k % 4]).translate((-1.6 + 0.4 * k, 0.6, -0.3 * (k % 3))).animate_moving(v))
+    cam = (R.Camera.build().vertical_fov(40.0, 9.0 / 16.0).position((0.3, 1.2, 5.0)).look_at((0, 1, 0), (0, 0.5, 0))
+           .motion_blur(0.0, 1.0).build())
+    world = g.build().finish(wb, R.BackgroundColor.sky(), cam)
+    world.raw.camera.shutter_pace[0], world.raw.camera.shutter_pace[1] = pace
+    return world
+
+
+@pytest.mark.parametrize("pace", [(0.8, -0.6), (-1.5, 2.0)])
+def test_sah_rolling_shutter_motion(pace, monkeypatch):
+    """the SAH tree's boxes of Animation leaves sweep every ray time, the rolling
+    shutter's included (rtw_cull.h rtw_ray_time_range): bit-exact against the oracle and the
+    reference-tree loop with a non-zero shutter_pace."""
+    world = _rolling_shutter_world(pace)
+    assert _kernel_tree(world) == "sah"
+    size = R.Size2i(96, 54)
+    gpu = R.render(size, 1, 8, 50, world, seed=43)
+    assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=43)), f"rolling shutter {pace}")
+    big = R.Size2i(480, 270)
+    sah = R.render(big, 1, 4, 50, world, seed=43)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert_bit_identical(sah, R.render(big, 1, 4, 50, world, seed=43), f"rolling shutter {pace}, SAH vs reference")
+
+
 def test_sah_ties_and_grazing_hits(monkeypatch):
     world = _tie_world()
     assert _kernel_tree(world) == "sah"

@@ -4,8 +4,12 @@
   RTW_LIBRARY=$PWD/raytracinginaweekend_amd/librtw_pt.so python tools/phase_timing.py --scene final_scene1
 
 Phases (per wave, summed over waves; a wave's cycles include the time other waves on its SIMD
-issue): 1 refill (work items, camera rays), 2 traversal setup (the ray's reciprocals), 3 traversal,
-4 shading and colour stores.  The frame after a warm-up frame (cost order, tuned threshold).
+issue; the phase is switched by the wave's first active lane, so divergent sub-phases count whole-wave
+cycles): 1 refill (work items), 2 traversal setup (the ray's reciprocals), 3 traversal (SAH walk,
+drain, proof, re-traces), 4 shading (hit record, material, texture, pdf), 5 sample start (stream
+setup, jitter, camera ray and its UnitDisc), 6 shading's samplers (UnitSphere / UnitBall rejection
+loops, gen_bool, light direction), 7 colour store and cost bookkeeping.  The frame after a warm-up
+frame (cost order, tuned threshold).
 """
 import argparse
 import ctypes as C
@@ -42,9 +46,11 @@ def main():
     torch.cuda.synchronize()
     if fn(buf) != 0:
         raise SystemExit("library built without RTW_PHASE_TIMING")
-    names = {1: "refill + camera", 2: "traversal setup", 3: "traversal", 4: "shading + stores"}
+    names = {1: "refill", 2: "traversal setup", 3: "traversal", 4: "shading", 5: "sample start",
+             6: "samplers", 7: "stores"}
     tot = sum(buf[k] for k in names)
-    print(a.scene, " ".join(f"{names[k]} {buf[k] / tot:.3f}" for k in names))
+    print(a.scene, f"{a.width}x{a.height}x{a.spp}", " ".join(f"{names[k]} {buf[k] / tot:.4f}" for k in names),
+          f"(wave cycles {tot})", flush=True)
 
 
 if __name__ == "__main__":
