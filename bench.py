@@ -26,6 +26,10 @@ Extra fields:
                 (400x225x64) in full.
   first_frame_ms  one cold drop-in rtw_render of the configured frame (upload, tuning frame in
                 chunk-major order, copy back): what a single reference-style render call costs.
+  configs       N = 1 only: the other BASELINE configs on this GPU -- suzanne 1080p512 (C4),
+                cornell_cube 800x800x1024 (C3), earth_motion 3840x2160x2048 (C5) -- each 1 warm-up +
+                --configs-steps timed frames (HIP events on the launch stream beside the wall clock),
+                with its own VALU-issue roofline, lane utilisation and HBM traffic from two PMC runs.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (--gpus N > 1 without torchrun: starts N rank processes itself, before any GPU call)
@@ -65,11 +69,9 @@ def alg_bytes(stats: dict, pixels: int) -> int:
     )
 
 
-def _pmc_pass(args, counters) -> dict | None:
-    """One `rocprofv3 --pmc <counters>` run of this benchmark (1 warm-up + 1 timed frame, no extra
-    legs): per counter, the sum over the timed frame's render_kernel dispatches (the last half of
-    them; counters of one dispatch may come as several rows), plus that frame's dispatch time
-    from the trace timestamps.  None if rocprofv3 is unavailable or the pass fails."""
+def _pmc_rows(child_args: list, counters) -> list | None:
+    """The render_kernel rows of one `rocprofv3 --pmc <counters>` run of this benchmark with
+    `child_args`.  None if rocprofv3 is unavailable or the pass fails."""
     import csv
     import glob
     import shutil
@@ -78,10 +80,7 @@ def _pmc_pass(args, counters) -> dict | None:
 
     if not shutil.which("rocprofv3"):
         return None
-    child = [sys.executable, os.path.abspath(__file__), "--scene", args.scene, "--width", str(args.width), "--height",
-             str(args.height), "--spp", str(args.spp), "--max-depth", str(args.max_depth), "--seed", str(args.seed),
-             "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-stats", "--no-pmc", "--no-first-frame",
-             "--no-thread-count"]
+    child = [sys.executable, os.path.abspath(__file__)] + child_args
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
         cmd = ["rocprofv3", "--pmc", *counters, "-d", d, "-o", "pmc", "--output-format", "csv", "--"] + child
         try:
@@ -91,6 +90,13 @@ def _pmc_pass(args, counters) -> dict | None:
         rows = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             rows += [r for r in csv.DictReader(open(f)) if "render_kernel" in r["Kernel_Name"]]
+    return rows or None
+
+
+def _pmc_reduce(rows) -> dict | None:
+    """Per counter, the sum over the timed frame's render_kernel dispatches among `rows` (a warm-up
+    and a timed frame with the same launch count: the last half of the dispatches; counters of one
+    dispatch may come as several rows), plus that frame's dispatch time from the trace timestamps."""
     if not rows:
         return None
     ids = sorted({int(r["Dispatch_Id"]) for r in rows})
@@ -104,6 +110,14 @@ def _pmc_pass(args, counters) -> dict | None:
         span[r["Dispatch_Id"]] = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
     got["dispatch_ns"] = sum(e - s for s, e in span.values())
     return got
+
+
+def _pmc_pass(args, counters) -> dict | None:
+    """One PMC run of this benchmark's headline workload (1 warm-up + 1 timed frame, no extra legs)."""
+    child = ["--scene", args.scene, "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
+             "--max-depth", str(args.max_depth), "--seed", str(args.seed), "--steps", "1", "--warmup", "1",
+             "--no-cpu-baseline", "--no-stats", "--no-pmc", "--no-first-frame", "--no-thread-count", "--no-configs"]
+    return _pmc_reduce(_pmc_rows(child, counters))
 
 
 def pmc_traffic(args) -> dict | None:
@@ -125,6 +139,98 @@ def pmc_valu(args) -> dict | None:
     if not c or any(k not in c for k in VALU_COUNTERS):
         return None
     return c
+
+
+# The other BASELINE configs, on one GPU (the headline is configs[1], final_scene1 1080p512)
+CONFIG_LEGS = (
+    ("suzanne", 1920, 1080, 512, "C4 (BASELINE configs[3], suzanne.obj + BVH, 1080p512) on one GPU"),
+    ("cornell_cube", 800, 800, 1024, "C3 (BASELINE configs[2], Cornell box + cube.obj, 800x800x1024)"),
+    ("earth_motion", 3840, 2160, 2048, "C5 (BASELINE configs[4], earthmap + motion blur, 4Kx2048) on one GPU"),
+)
+
+
+def _kernel_tag(v: dict) -> str:
+    """The render kernel's name fragment in rocprofv3's Kernel_Name for a kernel_variant() dict."""
+    return f"render_kernel<false, {v['lds_mode']}, {v['leaf_kinds']}, {v['tex_kinds']}>"
+
+
+def render_configs(args, local_rank: int, steps: int, warmup: int, barrier) -> list:
+    """`warmup` untimed + `steps` timed frames of each CONFIG_LEGS workload on this GPU (each world
+    released before the next: the C5 frame's colour buffer takes up to 64 GiB)."""
+    import gc
+
+    import torch
+
+    import raytracinginaweekend_amd as R
+    from raytracinginaweekend_amd.distributed import FrameRenderer, FrameSpec
+
+    out = []
+    for name, w, h, spp, label in CONFIG_LEGS:
+        world = R.demo_world(name)
+        fr = FrameRenderer(world, FrameSpec(R.Size2i(w, h), spp, args.max_depth, args.seed), 0, 1, local_rank)
+        for _ in range(warmup):
+            fr.launch()
+        barrier()
+        rec = {"workload": f"{name} {w}x{h}x{spp}spp max_depth {args.max_depth}", "baseline_config": label}
+        if steps > 0:
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t = time.perf_counter()
+            st.record()
+            for _ in range(steps):
+                fr.launch()
+            en.record()
+            barrier()
+            dt = (time.perf_counter() - t) / steps
+            rec.update({"value": round(w * h * spp / dt / 1e6, 3), "unit": "Msamples/sec", "steps": steps,
+                        "warmup": warmup, "ms_per_step": round(dt * 1e3, 3),
+                        "kernel_ms": round(st.elapsed_time(en) / steps, 3)})
+        rec.update({"trace_min": fr.dworld.tuned_trace_min(), "kernel": fr.dworld.kernel_variant()})
+        out.append(rec)
+        fr.dworld.release()
+        del fr, world
+        gc.collect()
+    return out
+
+
+def configs_pmc(args, legs: list, peak_ginstr: float) -> None:
+    """PMC passes over all CONFIG_LEGS at once (a child renders 1 warm-up + 1 timed frame of each):
+    the VALU issue counters with WRITE_SIZE, then FETCH_SIZE (x2, gfx950) in a second run; rows are
+    told apart by the configs' kernel variants (distinct names required)."""
+    child = ["--configs-child", "--max-depth", str(args.max_depth), "--seed", str(args.seed)]
+    tags = [_kernel_tag(r["kernel"]) for r in legs]
+    if len(set(tags)) != len(tags):
+        for r in legs:
+            r["roofline"] = None
+            r["pmc_note"] = "configs share a kernel variant: their PMC rows cannot be told apart"
+        return
+    a = _pmc_rows(child, list(VALU_COUNTERS) + ["WRITE_SIZE"])
+    b = _pmc_rows(child, ["FETCH_SIZE"]) if a else None
+    for r, tag in zip(legs, tags):
+        v = _pmc_reduce([x for x in a or [] if tag in x["Kernel_Name"]])
+        f = _pmc_reduce([x for x in b or [] if tag in x["Kernel_Name"]])
+        if not v or any(k not in v for k in VALU_COUNTERS) or not r.get("kernel_ms"):
+            r["roofline"] = None
+            continue
+        k_s = r["kernel_ms"] * 1e-3
+        achieved = v["SQ_INSTS_VALU"] / k_s / 1e9
+        rl = {"bound": "valu_issue", "achieved": round(achieved, 1), "peak": round(peak_ginstr, 1),
+              "unit": "G VALU wave-instr/s", "frac": round(achieved / peak_ginstr, 4),
+              "insts_per_frame": int(v["SQ_INSTS_VALU"]),
+              "lane_utilisation": round(v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"]), 4),
+              "wait_any_frac": round(v["SQ_WAIT_ANY"] / v["SQ_WAVE_CYCLES"], 4),
+              "launches_per_frame": v["launches"]}
+        write = v.get("WRITE_SIZE", 0.0) * 1024.0
+        if f and "FETCH_SIZE" in f:
+            fetch = f["FETCH_SIZE"] * 1024.0 * 2.0
+            rl["traffic"] = round(fetch + write)
+            rl["hbm_GBps"] = round((fetch + write) / k_s / 1e9, 1)
+            rl["hbm_frac"] = round((fetch + write) / k_s / 1e9 / HBM_PEAK_GBS, 5)
+            rl["traffic_detail"] = {"fetch_bytes_x2": round(fetch), "write_bytes": round(write),
+                                    "colour_record_bytes": r["colour_record_bytes"]}
+        rl["source"] = ("rocprofv3 --pmc " + " ".join(VALU_COUNTERS) + " WRITE_SIZE, then FETCH_SIZE, on a child "
+                        "rendering 1 warm-up + 1 timed frame of each config; achieved = SQ_INSTS_VALU / this leg's "
+                        "kernel_ms")
+        r["roofline"] = rl
 
 
 def _cpu_info() -> dict:
@@ -271,6 +377,9 @@ def main() -> int:
     ap.add_argument("--no-traffic", action="store_true", help="skip only the HBM traffic passes")
     ap.add_argument("--no-first-frame", action="store_true")
     ap.add_argument("--no-thread-count", action="store_true", help="skip the thread_count = available_parallelism leg")
+    ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (C3, C4, C5 on one GPU)")
+    ap.add_argument("--configs-steps", type=int, default=3, help="timed frames per config of that leg")
+    ap.add_argument("--configs-child", action="store_true", help=argparse.SUPPRESS)  # the configs' PMC passes
     ap.add_argument("--thread-count-leg", type=int, default=0, help="thread_count of that leg (0: available_parallelism)")
     ap.add_argument("--stats-spp", type=int, default=128, help="spp of the counting render (scaled to --spp)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -300,15 +409,19 @@ def main() -> int:
     import raytracinginaweekend_amd as R
     from raytracinginaweekend_amd.distributed import FrameRenderer, FrameSpec
 
-    world = R.demo_world(args.scene)
-    spec = FrameSpec(R.Size2i(args.width, args.height), args.spp, args.max_depth, args.seed)
-    fr = FrameRenderer(world, spec, rank, world_size, local_rank)
-
     def barrier():
         torch.cuda.synchronize(dev)
         if world_size > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
+
+    if args.configs_child:  # a PMC pass of the configs leg: 1 warm-up + 1 profiled frame each, no line
+        render_configs(args, local_rank, 1, 1, barrier)
+        return 0
+
+    world = R.demo_world(args.scene)
+    spec = FrameSpec(R.Size2i(args.width, args.height), args.spp, args.max_depth, args.seed)
+    fr = FrameRenderer(world, spec, rank, world_size, local_rank)
 
     for _ in range(args.warmup):
         fr.render_frame()
@@ -368,7 +481,9 @@ def main() -> int:
             "counts": f"counting variant of the timed kernel's traversal at {sp.samples_per_pixel} spp, scaled x{scale:g}",
             "note": "SURVEY §8(d) record bytes (32 B per node or leaf-box visit, the primitive records, material and "
                     "texel reads, the framebuffer) / kernel time; the records come from LDS and L2, so they are "
-                    "priced against the LDS array peak (256 B/clk/CU), not HBM (HBM: see traffic)",
+                    "priced against the LDS array peak (256 B/clk/CU), not HBM (HBM: see traffic); approximate "
+                    "where the product kernel traces cooperatively: the counting variant re-traces tied rays on "
+                    "the reference tree and walks the drain's last rays (DESIGN 5.7)",
             "per_sample": {k: round(v / max(1, stats["samples"]), 3) for k, v in stats.items() if k != "samples"},
         }
 
@@ -429,6 +544,14 @@ def main() -> int:
                           "as merge_planes (rendering.rs:222-252) on the device; 2 frames after a warm-up"}
         del fr_t
 
+    configs = None
+    if rank == 0 and world_size == 1 and not args.no_configs:
+        configs = render_configs(args, local_rank, max(1, args.configs_steps), 1, barrier)
+        for (name, w, h, spp, _), r in zip(CONFIG_LEGS, configs):
+            r["colour_record_bytes"] = w * h * spp * 12
+        if not args.no_pmc:
+            configs_pmc(args, configs, peak_ginstr)
+
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -470,6 +593,7 @@ def main() -> int:
             if first_frame_ms else None,
             "roofline": roofline,
             "thread_count_leg": tc_leg,
+            "configs": configs,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

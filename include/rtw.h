@@ -285,7 +285,9 @@ RTW_API int rtw_render_collect_stats(rtw_gpu_world* gw, const rtw_render_params*
                                      rtw_render_stats* stats);
 /* The same counts for the traversal the product kernel runs (tree 1): on worlds that take the SAH
  * walk, its node and leaf visits plus the leaf-box proof and the re-traced rays; elsewhere as
- * tree 0 (= rtw_render_collect_stats).  No reference counterpart: feeds the measured record bytes. */
+ * tree 0 (= rtw_render_collect_stats).  Approximate where the product kernel uses its wave-
+ * cooperative trace: the counting variant re-traces tied rays on the reference tree and
+ * walks the drain's last rays instead.  No reference counterpart: feeds the measured record bytes. */
 RTW_API int rtw_render_collect_stats_tree(rtw_gpu_world* gw, const rtw_render_params* params, int tree,
                                           rtw_render_stats* stats);
 /* Profiling aid (no reference counterpart): the statistics render plus up to n wave-level

@@ -298,7 +298,22 @@ RTW_HD uint32_t rtw_gen_range_u32(uint32_t n, rtw_xoro* r) {
  *   logf    sysdeps/ieee754/flt-32/e_logf.c + e_logf_data.c             (f64 kernel, FMA build)
  * The FMA builds contract specific multiply-adds; each rtw_fma below marks one of them.  Pinned
  * exhaustively against the live libm (tests/native/libm_check.c: every f32 input of acosf, sinf
- * and logf, 2^28 atan2f pairs; 0 mismatches) and by tests/golden/libm_f32.npz. */
+ * and logf, 2^28 atan2f pairs; 0 mismatches) and by tests/golden/libm_f32.npz.
+ *
+ * Notices of the restated algorithms (their coefficients and operation order are reproduced below):
+ *
+ *   rtw_acosf, rtw_atan2f (e_acosf.c, e_atan2f.c, s_atanf.c; fdlibm, converted to float by Ian Lance
+ *   Taylor, Cygnus Support):
+ *     Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ *     Developed at SunPro, a Sun Microsystems, Inc. business.
+ *     Permission to use, copy, modify, and distribute this software is freely granted, provided that
+ *     this notice is preserved.
+ *
+ *   rtw_sinf, rtw_logf (s_sinf.c, sincosf.h, sincosf_data.c, e_logf.c, e_logf_data.c): written by
+ *   Szabolcs Nagy and others for Arm's optimized-routines (Copyright (c) 2017-2018, Arm Limited;
+ *   SPDX-License-Identifier: MIT) and contributed to the GNU C Library (Copyright (C) 2017-2022 Free
+ *   Software Foundation, Inc.; the GNU C Library is free software, distributed under the GNU Lesser
+ *   General Public License, version 2.1 or any later version). */
 RTW_HD double rtw_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 /* e_acosf.c __ieee754_acosf */

@@ -32,5 +32,11 @@ hipError_t sort_pairs_desc(const uint32_t* keys_in, uint32_t* keys_out, const ui
 // children encoded as in rtw_bvh_node (>= 0 node, < 0 leaf -1 - index).  *depth = nodes on the
 // longest root-to-leaf path (rtw_sah.cpp).
 int sah_build(const float* lo, const float* hi, int32_t n, std::vector<rtw_bvh_node>& nodes, int32_t* root, int* depth);
+// The same with spatial splits (rtw_sah.cpp): tri = 9 floats per leaf (vertices; x = NaN: not a
+// triangle, cut as a box), leaf_km = {k, m} per leaf (k < 0: never hits), at most budget x n extra
+// references.  Node boxes are the unions of the references' clipped boxes below (rounded outward);
+// km = 2 floats per node, the maxima of the leaf constants below.
+int sah_build_split(const float* lo, const float* hi, const float* tri, const float* leaf_km, int32_t n, double budget,
+                    std::vector<rtw_bvh_node>& nodes, std::vector<float>& km, int32_t* root, int* depth);
 
 }  // namespace rtw

@@ -1,17 +1,21 @@
 // rtw_device.hip -- the MI355X (gfx950) path-tracing megakernel and its C ABI.
 //
-// Hot path restated for the device (reference: src/lib/rendering.rs:19-220):
-//   one wave = 64 pixels of one image tile; one lane = one pixel, iterating its samples in
-//   order (so the per-pixel f32 sum is the reference's sequential `.sum::<Color>()`,
-//   rendering.rs:172-179); a finished path immediately regenerates the lane's next camera
-//   sample, so a wave keeps every lane busy until its pixels' sample budgets are spent.
-//   BVH traversal is iterative with a per-lane stack in LDS, visiting nodes in exactly the
-//   reference's recursive order (hittable.rs:429-462: per-axis slab test with the CURRENT
-//   t_range, near child first by ray.direction[axis] > 0, both children always visited).
-//   Candidate tests compute only `t`; the hit record (position / normal / uv / front_face) is
-//   rebuilt once for the closest leaf -- a pure function of (leaf, ray, t), so it equals the
-//   record the reference builds eagerly.  Volumes draw their RNG during traversal in the same
-//   order as the reference.
+// Hot path restated for the device (reference: src/lib/rendering.rs:19-220; DESIGN.md §5):
+//   a persistent kernel, one 1024-thread block per CU with the scene (nodes, leaf records, cull
+//   constants, shading tables) staged in LDS.  Each lane runs a state machine PIXEL -> TRACE ->
+//   SHADE over work items taken from 16 queues in per-wave batches: an item is one (pixel, sample)
+//   -- or, with whole-pixel items, all of a pixel's samples -- and its colour goes to a per-sample
+//   buffer that accumulate_kernel sums per pixel in sample order (the reference's sequential
+//   `.sum::<Color>()`, rendering.rs:172-179), so the image does not depend on which lane, wave or
+//   GPU rendered a sample (one RNG stream per (pixel, sample)).
+//   Closest hits are found on the kernel's own SAH tree (2- or 4-wide) with the proximity cull
+//   alone, then proven to be the reference DFS's answer (hittable.rs:429-473) with one slab test on
+//   the leaf's parent box in the reference tree; rays the proof does not cover are re-traced on the
+//   reference tree in the reference's order (near child first by ray.direction[axis] > 0, both
+//   children, te shrinking).  Ties are resolved by the leaves' reference DFS keys (coop_trace).
+//   Candidate tests compute only `t`; the hit record is rebuilt once for the closest leaf -- a pure
+//   function of (leaf, ray, t).  Volumes draw their RNG during traversal in the reference's order
+//   (their worlds keep the reference tree).
 //
 // Scene data lives in one HBM arena as SoA float4 streams (see DESIGN.md "Data layout").
 // Numerics: -ffp-contract=off, no fast-math; shared scalar spec in include/rtw_scalar.h.
@@ -116,6 +120,13 @@ struct DWorld {
     // per axis the bits of the ancestors splitting on it}, bit 31 - k for the ancestor at depth k;
     // null when the reference tree is deeper than 32
     const uint4* leaf_key;
+    // the SAH tree collapsed to four children per node (plain-sphere worlds, traverse4): per node 4 child
+    // records {min.xyz, max.x} (a leaf child: its sphere {c, r}), 4 {max.y, max.z, k, m} and the children
+    // {c0..c3} (>= 0 node, -1 - leaf, RTW_Q4_EMPTY none)
+    const float4* sah4_a;
+    const float4* sah4_b;
+    const int4* sah4_c;
+    int32_t sah4_root;
     int32_t sah_root;
     int32_t root;
     int32_t has_light;
@@ -208,12 +219,18 @@ struct KArgs {
     // solid-texture worlds, each texture's first record; the stack follows them (stack_off)
     int32_t sh_li, sh_mat, sh_tex0, stack_off;
     int32_t material_count, texture_count;
+    int32_t sah4;             // 1: the SAH walk runs on the 4-wide tree (node_count = its nodes; traverse4)
+    int32_t fast_off;         // LDS float4 offset of the leaf records (leaf_fast)
     int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
                               // re-traced on the reference tree where the proof does not hold (§5.6)
     int32_t coop_max;         // drain: a wave with at most this many live lanes traces each ray with all
                               // 64 lanes over every leaf (coop_trace); 0: never
     int32_t coop_ties;        // 1: the walk's tied rays are resolved by coop_trace (else re-traced); 2: audit
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
+    // 1: a work item is a whole pixel (all spp samples of a slot, one lane, in sample order): the lane
+    // sums the colours in registers -- the reference's sequential .sum(), rendering.rs:172-179 -- and
+    // writes sum / spp to `out` itself; no colour buffer, no accumulation kernel (thread_count 1)
+    int32_t whole_pixel;
     // work order by measured cost (render_frame): costlier tiles first, all their samples together
     const uint32_t* tile_perm;  // tile rank -> local tile, null: chunk-major order
     uint32_t* slot_cost;        // per slot: bounces of the deep (> 3 bounce) paths rendered there
@@ -1422,7 +1439,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     auto take = [&](float t, int leaf) {
         if (TM == TM_SAH) {
             // selects, not branches (+1.6 % on final_scene1: the branchy form cost exec-mask work)
-            const bool tie = T.found >= 0 && t == __int_as_float(__float_as_int(T.te) - 1);
+            // (a leaf referenced twice -- a spatial split of the SAH tree, rtw_sah.cpp -- meets itself: no tie)
+            const bool tie = T.found >= 0 && T.found != leaf && t == __int_as_float(__float_as_int(T.te) - 1);
             T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
             T.te = tie ? T.te : __int_as_float(__float_as_int(t) + 1);  // t >= 0.001: the next float up
             T.found = tie ? T.found : leaf;
@@ -1642,6 +1660,120 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     return T;
 }
 
+// The SAH walk of plain-sphere worlds on the tree collapsed to four children per node:
+// a lane stands on an accepted node (the root, or a child accepted by its parent's step); its step
+// tests the node's leaf children's spheres first (their hits shrink te), then its internal children's
+// grown boxes (node_pass_cons), moves to the accepted child whose grown box the segment enters first
+// and pushes the other accepted ones.  Against the two-children walk it skips the boxes of every
+// other level and runs half the steps (the step's loop, stack and mask work are per step); the node's
+// nine records are loaded at once, none depends on another.  Step 1 of DESIGN 5.5 holds for any tree
+// whose boxes contain their leaves' accepted points (within delta): the closest root and the tie flag
+// are the two-children walk's.
+#define RTW_Q4_EMPTY ((int32_t)0x80000000)
+#ifndef RTW_Q4_UNROLL
+#define RTW_Q4_UNROLL 2
+#endif
+template <bool STATS>
+__device__ __forceinline__ Trav traverse4(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n4,
+                                       int32_t stack_off, unsigned long long* dbg, int32_t coop_exit) {
+    (void)wp;
+    int32_t off_b = 4 * n4, off_c = 8 * n4;
+    asm volatile("" : "+v"(off_b), "+v"(off_c));
+    const float4* qa = smem;
+    const float4* qb = smem + off_b;
+    const int4* qc = reinterpret_cast<const int4*>(smem + off_c);
+    int32_t* stack = reinterpret_cast<int32_t*>(smem + stack_off) + threadIdx.x;
+    auto take = [&](float t, int leaf) {  // as the two-children walk's (traverse, TM_SAH)
+        const bool tie = T.found >= 0 && T.found != leaf && t == __int_as_float(__float_as_int(T.te) - 1);
+        T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
+        T.te = tie ? T.te : __int_as_float(__float_as_int(t) + 1);
+        T.found = tie ? T.found : leaf;
+    };
+    const RayPre rp{T.inv, true};
+    Stats st;
+    if (STATS)
+        for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
+    (void)dbg;
+    for (;;) {
+        const unsigned long long tr = __ballot(T.phase == PH_TRACE);
+        if (tr == 0) break;
+        if ((uint32_t)__popcll(tr) < (uint32_t)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
+        if ((int32_t)__popcll(tr) <= coop_exit) break;
+#pragma unroll
+        for (int u = 0; u < (STATS ? 1 : RTW_Q4_UNROLL); ++u) {
+            if (T.phase == PH_TRACE) {
+                const int32_t base = 4 * T.node;
+                const int4 ch = qc[T.node];
+                const int32_t c[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (c[j] < 0 && c[j] != RTW_Q4_EMPTY) {
+                        if (STATS) st.c[ST_T_SPHERE]++;
+                        float t;
+                        if (sphere_t(qa[base + j], T.ray, 0.001f, T.te, t)) take(t, -1 - c[j]);
+                    }
+                }
+                float be = F32_INF;
+                int32_t bn = -1;
+                float e[4];
+                bool acc[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[j] = false;
+                    e[j] = F32_INF;
+                    if (c[j] >= 0) {
+                        if (STATS) st.c[ST_NODES]++;
+                        const float4 b = qb[base + j];
+                        acc[j] = node_pass_cons<false>(qa[base + j], b, make_float2(b.z, b.w), T.ray, rp, 0.001f, T.te, e[j]);
+                    }
+                    const bool nearer = acc[j] && e[j] < be;
+                    be = nearer ? e[j] : be;
+                    bn = nearer ? c[j] : bn;
+                }
+                // the other accepted children go on the stack, the farthest first (popped last)
+                float k[4];
+                int32_t v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool push = acc[j] && c[j] != bn;
+                    k[j] = push ? e[j] : -F32_INF;
+                    v[j] = c[j];
+                }
+                auto cx = [&](int a, int b) {  // descending by key
+                    const bool sw = k[a] < k[b];
+                    const float ka = k[a], kb = k[b];
+                    const int32_t va = v[a], vb = v[b];
+                    k[a] = sw ? kb : ka;
+                    k[b] = sw ? ka : kb;
+                    v[a] = sw ? vb : va;
+                    v[b] = sw ? va : vb;
+                };
+                cx(0, 1);
+                cx(2, 3);
+                cx(0, 2);
+                cx(1, 3);
+                cx(1, 2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (k[j] > -F32_INF) stack[(T.sp++) * RTW_BLOCK] = v[j];
+                if (bn >= 0) {
+                    T.node = bn;
+                } else if (T.sp == 0) {
+                    T.phase = PH_SHADE;
+                } else {
+                    T.node = stack[(--T.sp) * RTW_BLOCK];
+                }
+            }
+        }
+    }
+    if (STATS) {
+        T.n_nodes = st.c[ST_NODES];
+        T.n_sph_rect = st.c[ST_T_SPHERE];
+        T.n_box_tri = 0;
+    }
+    return T;
+}
+
 // The frame's drain (§5.7): once the queues are empty a wave's last paths run alone, and a path
 // trapped inside suzanne's mesh walks nearly every node and triangle on each of its ~50 bounces
 // (~15 ms on one lane, the 8-GPU shares' tail).  When at most coop_max lanes are still live, each
@@ -1660,14 +1792,14 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 // the DFS-last tied leaf instead: wrong images, which shows that the resolution decides them.
 template <int LDS, int LK>
 __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, unsigned long long todo, int32_t n_nodes,
-                                        int32_t n_leaves, int32_t n_rects, bool audit) {
+                                        int32_t n_leaves, int32_t n_rects, int32_t fast_off, bool audit) {
     const DWorld& w = *wp;
     constexpr bool LDS_SCENE = LDS >= 1;
     const int32_t rect_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
     const int32_t tri_off = rect_off + 2 * n_rects;
     const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
     const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
-    const float4* fast = LDS_SCENE ? smem + 2 * n_nodes : uniform_ptr(w.leaf_fast);
+    const float4* fast = LDS_SCENE ? smem + fast_off : uniform_ptr(w.leaf_fast);
     const int lane = threadIdx.x & 63;
     const uint4* keys = uniform_ptr(w.leaf_key);
     while (todo) {  // wave-uniform: one ray at a time
@@ -1748,7 +1880,27 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     // asked for the product kernel's own traversal (stats_tree 1; else the reference's statistics)
     constexpr bool SAHK = LK <= LK_WRAPPED;
     const bool sah = SAHK && A.sah != 0;
-    if (LDS_SCENE) {
+    if (LDS_SCENE && sah && LK == LK_SPHERES && A.sah4) {
+        // the 4-wide tree: [child records a 4n][child records b 4n][children n][leaf records L]
+        const int32_t n4 = A.node_count;
+        for (int i = threadIdx.x; i < 4 * n4; i += RTW_BLOCK) {
+            smem[i] = w.sah4_a[i];
+            smem[4 * n4 + i] = w.sah4_b[i];
+        }
+        for (int i = threadIdx.x; i < n4; i += RTW_BLOCK) reinterpret_cast<int4*>(smem)[8 * n4 + i] = w.sah4_c[i];
+        for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[A.fast_off + i] = w.leaf_fast[i];
+        if (A.sh_li >= 0) {
+            int4* li = reinterpret_cast<int4*>(smem + A.sh_li);
+            for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) li[i] = w.leaf_info[i];
+            int4* mt = reinterpret_cast<int4*>(smem + A.sh_mat);
+            for (int i = threadIdx.x; i < A.material_count; i += RTW_BLOCK) mt[i] = w.materials[i];
+            if (A.sh_tex0 >= 0) {
+                int4* tx = reinterpret_cast<int4*>(smem + A.sh_tex0);
+                for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
+            }
+        }
+        __syncthreads();
+    } else if (LDS_SCENE) {
         const float4* ga = sah ? w.sah_a : w.node_a;
         const float4* gb = sah ? w.sah_b : w.node_b;
         const float2* gk = sah ? w.sah_km : w.node_km;
@@ -1779,7 +1931,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     }
     // the traversal stacks follow the LDS scene and the shading tables
     const int32_t stack_off = LDS_SCENE ? A.stack_off : 0;
-    const ShadeTabs stabs{A.sh_li, A.sh_mat, A.sh_tex0, A.sh_li >= 0 ? 2 * A.node_count : -1};
+    const ShadeTabs stabs{A.sh_li, A.sh_mat, A.sh_tex0, A.sh_li >= 0 ? A.fast_off : -1};
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
@@ -1794,6 +1946,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     uint32_t sample = 0, sample_end = 0;
     float pdot = 0.0f;  // dot((0,1,0), primary ray direction): the background's argument
     V3 att = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
+    V3 psum = v3(0.0f, 0.0f, 0.0f);  // whole-pixel items: the pixel's running sum
     int32_t depth = 0;
     Trav T;
     T.phase = PH_PIXEL;
@@ -1978,6 +2131,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         fy = (float)py * A.sy;
                         sample = big ? A.s_begin + ck * A.chunk : A.s_split + ck;
                         sample_end = big ? min(sample + A.chunk, A.s_split) : sample + 1;
+                        psum = v3(0.0f, 0.0f, 0.0f);
                         start_sample(1);
                         T.phase = PH_TRACE;
                     }
@@ -2008,7 +2162,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             T.node = w.root;
             if (sah) {  // the SAH walk needs the exact fast division; other rays take the reference tree
                 if (rp.fast) {
-                    T.node = w.sah_root;
+                    T.node = LK == LK_SPHERES && A.sah4 ? w.sah4_root : w.sah_root;
                     T.fast |= RTW_TF_SAH;
                 } else {
                     T.phase = PH_REF;
@@ -2031,9 +2185,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 #ifdef RTW_WAVE_TIMING
             uint64_t wx_t0 = wall_clock64();
 #endif
-            T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
-                                                       A.leaf_count, A.rect_count, A.tri_count, stack_off,
-                                                       STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
+            if (LDS_SCENE && LK == LK_SPHERES && A.sah4)
+                T = traverse4<STATS>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, stack_off,
+                                     STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
+            else
+                T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
+                                                           A.leaf_count, A.rect_count, A.tri_count, stack_off,
+                                                           STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
             // the rays coop_trace takes (one call site, inlined: as an out-of-line call taking and
             // returning Trav by value it cost 304 B of scratch per lane, saved and restored around
             // every call -- suzanne's and cornell_cube's extra write traffic): the drain's last rays
@@ -2053,7 +2211,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             if (!STATS && LK <= LK_PLAIN && A.coop_ties)
                 coop |= __ballot(T.phase == PH_SHADE && (T.fast & (RTW_TF_SAH | RTW_TF_TIE)) == (RTW_TF_SAH | RTW_TF_TIE));
             if (!STATS && LK <= LK_PLAIN && coop)
-                T = coop_trace<LDS, LK>(A.wdev, T, coop, A.node_count, A.leaf_count, A.rect_count, A.coop_ties == 2);
+                T = coop_trace<LDS, LK>(A.wdev, T, coop, A.node_count, A.leaf_count, A.rect_count, A.fast_off, A.coop_ties == 2);
 #ifdef RTW_WAVE_TIMING
             const uint64_t wx_t1 = wall_clock64();
             if (qfail >= RTW_QUEUES) wx_tcoop += wx_t1 - wx_t0;
@@ -2158,10 +2316,14 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             T.phase = PH_TRACE;
             if (so.done) {
                 RTW_PT(7);
-                float* o = A.colors + ((uint64_t)(sample - A.s_begin) * A.total + slot) * 3;
-                o[0] = so.color.x;
-                o[1] = so.color.y;
-                o[2] = so.color.z;
+                if (A.whole_pixel) {
+                    psum = add(psum, so.color);  // in sample order: this lane renders the pixel's samples in turn
+                } else {
+                    float* o = A.colors + ((uint64_t)(sample - A.s_begin) * A.total + slot) * 3;
+                    o[0] = so.color.x;
+                    o[1] = so.color.y;
+                    o[2] = so.color.z;
+                }
                 if (STATS) st.c[ST_SAMPLES]++;
                 // deep paths (rare: trapped inside meshes, up to ~100x the mean cost) mark their
                 // slot for the next frame's work order
@@ -2175,8 +2337,18 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 }
 #endif
                 ++sample;
-                if (sample >= sample_end) T.phase = PH_PIXEL;
-                else start_sample(7);
+                if (sample >= sample_end) {
+                    T.phase = PH_PIXEL;
+                    if (A.whole_pixel) {  // accumulate_kernel's last step, for this pixel
+                        const V3 px = divs(psum, (float)A.spp);
+                        float* o = A.layout == RTW_LAYOUT_TILES ? A.out + 3 * (size_t)slot : A.out + 3 * (size_t)pix;
+                        o[0] = px.x;
+                        o[1] = px.y;
+                        o[2] = px.z;
+                    }
+                } else {
+                    start_sample(7);
+                }
             } else {
                 fresh = true;  // the scattered ray continues the path
             }
@@ -2650,6 +2822,10 @@ struct SahTables {
     std::vector<float> km;        // cull constants, 2 per node
     std::vector<float4> box;      // 2 per leaf: the proof box (the leaf's parent box in the reference tree)
     std::vector<uint4> key;       // per leaf: its DFS key material (DWorld::leaf_key), empty if too deep
+    // the tree collapsed to 4 children per node (plain-sphere worlds; DWorld::sah4_*), empty if not made
+    std::vector<float4> a4, b4;
+    std::vector<int4> c4;
+    int32_t root4 = -1;
     int32_t root = 0, depth = 0;
     bool ok = false;
 };
@@ -2660,7 +2836,7 @@ SahTables build_sah_tables(const rtw_world* w) {
     const int32_t L = w->leaf_count;
     if (L < 2 || w->root < 0 || w->node_count < 1) return S;
     auto coord_ok = [](float c) { return c == 0.0f || (std::fabs(c) >= 0x1p-60f && std::fabs(c) <= 1073741824.0f); };
-    std::vector<float> lo((size_t)L * 3), hi((size_t)L * 3);
+    std::vector<float> lo((size_t)L * 3), hi((size_t)L * 3), lkm((size_t)L * 2);
     std::vector<uint8_t> never((size_t)L, 0);
     for (int32_t i = 0; i < L; ++i) {
         float k, m;
@@ -2669,6 +2845,8 @@ SahTables build_sah_tables(const rtw_world* w) {
         float* mx = &hi[3 * (size_t)i];
         if (!rtw_cull_leaf(w, &w->leaves[i], 1, &k, &m, mn, mx, &nv)) return S;
         never[(size_t)i] = (uint8_t)nv;
+        lkm[2 * (size_t)i] = nv ? -1.0f : k;
+        lkm[2 * (size_t)i + 1] = nv ? 0.0f : m;
         if (nv) {  // a leaf that never reports a hit: any box (it only has to sit somewhere in the tree)
             const rtw_triangle& t = w->triangles[w->leaves[i].geom_index];
             for (int k2 = 0; k2 < 3; ++k2) {
@@ -2697,14 +2875,43 @@ SahTables build_sah_tables(const rtw_world* w) {
     for (int32_t i = 0; i < L; ++i)
         if (parent[(size_t)i] < 0) return S;  // a leaf outside the reference tree
     std::vector<rtw_bvh_node> nodes;
-    if (rtw::sah_build(lo.data(), hi.data(), L, nodes, &S.root, &S.depth) != 0 || S.depth > RTW_STACK) return S;
-    // cull constants of the SAH tree over the leaves' true world boxes (wrapped leaves included)
-    rtw_world tw = *w;
-    tw.nodes = nodes.data();
-    tw.node_count = (int32_t)nodes.size();
-    tw.root = S.root;
-    S.km.assign(nodes.size() * 2, 0.0f);
-    rtw_cull_prepare_ex(&tw, S.km.data(), 0, 1);
+    // spatial splits (rtw::sah_build_split) in worlds with plain triangles, RTW_SAH_SPLIT_BUDGET extra
+    // references per leaf at most (0: the object-split tree)
+    double budget = 0.0;
+    if (const char* e = std::getenv("RTW_SAH_SPLIT_BUDGET")) budget = std::max(0.0, std::atof(e));
+    std::vector<float> tri;
+    if (budget > 0.0) {
+        tri.assign((size_t)L * 9, std::numeric_limits<float>::quiet_NaN());
+        bool any = false;
+        for (int32_t i = 0; i < L; ++i) {
+            const rtw_leaf& l = w->leaves[i];
+            if (l.geom_kind != RTW_GEOM_TRIANGLE || l.flags != 0 || never[(size_t)i]) continue;
+            const rtw_triangle& t = w->triangles[l.geom_index];
+            for (int v = 0; v < 3; ++v)
+                for (int k2 = 0; k2 < 3; ++k2) tri[9 * (size_t)i + 3 * v + k2] = t.positions[v][k2];
+            any = true;
+        }
+        if (!any) budget = 0.0;
+    }
+    if (budget > 0.0) {
+        // node boxes and cull constants come from the builder: a node's box is the union of its
+        // references' clipped boxes, k and m the maxima of the leaves' constants below
+        if (rtw::sah_build_split(lo.data(), hi.data(), tri.data(), lkm.data(), L, budget, nodes, S.km, &S.root, &S.depth) != 0 ||
+            S.depth > RTW_STACK)
+            return S;
+        for (const rtw_bvh_node& nd : nodes)
+            for (int k2 = 0; k2 < 3; ++k2)
+                if (!coord_ok(nd.min[k2]) || !coord_ok(nd.max[k2])) return S;
+    } else {
+        if (rtw::sah_build(lo.data(), hi.data(), L, nodes, &S.root, &S.depth) != 0 || S.depth > RTW_STACK) return S;
+        // cull constants of the SAH tree over the leaves' true world boxes (wrapped leaves included)
+        rtw_world tw = *w;
+        tw.nodes = nodes.data();
+        tw.node_count = (int32_t)nodes.size();
+        tw.root = S.root;
+        S.km.assign(nodes.size() * 2, 0.0f);
+        rtw_cull_prepare_ex(&tw, S.km.data(), 0, 1);
+    }
     for (float& c : S.km)  // x17/16 rounded up (inf stays inf): the cheap quotients' slack, node_pass_cons
         if (c > 0.0f) c = std::nextafter(c * RTW_SAH_WIDEN, std::numeric_limits<float>::infinity());
     S.a.resize(nodes.size());
@@ -2713,6 +2920,63 @@ SahTables build_sah_tables(const rtw_world* w) {
         const rtw_bvh_node& n = nodes[i];
         S.a[i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
         S.b[i] = make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
+    }
+    // 4-wide collapse for plain-sphere worlds (traverse4; RTW_SAH4=0 keeps the two-children walk): each
+    // node takes its two children and replaces the one with the largest box by its children until it has
+    // four (or only leaves); a leaf child's record is its sphere
+    bool spheres_only = true;
+    for (int32_t i = 0; i < L; ++i)
+        if (w->leaves[i].geom_kind != RTW_GEOM_SPHERE || w->leaves[i].flags != 0) spheres_only = false;
+    const char* e4 = std::getenv("RTW_SAH4");
+    if (spheres_only && (e4 && e4[0] == '1') && S.root >= 0) {
+        auto area = [&](int32_t n) {
+            const rtw_bvh_node& b = nodes[(size_t)n];
+            const double dx = (double)b.max[0] - b.min[0], dy = (double)b.max[1] - b.min[1], dz = (double)b.max[2] - b.min[2];
+            return dx * dy + dy * dz + dz * dx;
+        };
+        std::vector<std::pair<int32_t, int32_t>> todo{{S.root, 0}};  // (binary node, its 4-wide index)
+        S.c4.push_back(make_int4(0, 0, 0, 0));
+        S.a4.resize(4);
+        S.b4.resize(4);
+        S.root4 = 0;
+        while (!todo.empty()) {
+            const auto [n, q] = todo.back();
+            todo.pop_back();
+            std::vector<int32_t> ch{nodes[(size_t)n].left, nodes[(size_t)n].right};
+            while (ch.size() < 4) {
+                int best = -1;
+                double ba = -1.0;
+                for (size_t c = 0; c < ch.size(); ++c)
+                    if (ch[c] >= 0 && area(ch[c]) > ba) ba = area(ch[c]), best = (int)c;
+                if (best < 0) break;
+                const int32_t x = ch[(size_t)best];
+                ch.erase(ch.begin() + best);
+                ch.push_back(nodes[(size_t)x].left);
+                ch.push_back(nodes[(size_t)x].right);
+            }
+            int32_t cv[4] = {RTW_Q4_EMPTY, RTW_Q4_EMPTY, RTW_Q4_EMPTY, RTW_Q4_EMPTY};
+            for (size_t j = 0; j < ch.size(); ++j) {
+                const int32_t c = ch[j];
+                float4 ra = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rb = ra;
+                if (c < 0) {
+                    const rtw_sphere& sp = w->spheres[w->leaves[-1 - c].geom_index];
+                    ra = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius);
+                    cv[j] = c;
+                } else {
+                    const rtw_bvh_node& b = nodes[(size_t)c];
+                    ra = make_float4(b.min[0], b.min[1], b.min[2], b.max[0]);
+                    rb = make_float4(b.max[1], b.max[2], S.km[2 * (size_t)c], S.km[2 * (size_t)c + 1]);
+                    cv[j] = (int32_t)S.c4.size();
+                    todo.emplace_back(c, cv[j]);
+                    S.c4.push_back(make_int4(0, 0, 0, 0));
+                    S.a4.resize(S.a4.size() + 4);
+                    S.b4.resize(S.b4.size() + 4);
+                }
+                S.a4[4 * (size_t)q + j] = ra;
+                S.b4[4 * (size_t)q + j] = rb;
+            }
+            S.c4[(size_t)q] = make_int4(cv[0], cv[1], cv[2], cv[3]);
+        }
     }
     S.box.resize((size_t)L * 2);
     for (int32_t i = 0; i < L; ++i) {
@@ -2773,6 +3037,7 @@ struct rtw_gpu_world {
     int32_t tri_count = 0, rect_count = 0, material_count = 0, texture_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int32_t sah_nodes = 0;  // nodes of the SAH tree, 0: the world takes the reference tree only (§5.6)
+    int32_t sah4_nodes = 0; // nodes of its 4-wide collapse (plain-sphere worlds), 0: none
     int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
     int32_t tex_kinds = TX_ANY;   // TX_*: the texture code the world's textures need
     int cus = 0;
@@ -2987,6 +3252,10 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     const size_t o_sk = sah.ok ? L.push(sah.km.data(), sah.km.size() * sizeof(float)) : 0;
     const size_t o_lb = sah.ok ? L.push(sah.box.data(), sah.box.size() * sizeof(float4)) : 0;
     const size_t o_lk = sah.ok && !sah.key.empty() ? L.push(sah.key.data(), sah.key.size() * sizeof(uint4)) : 0;
+    const bool q4 = sah.ok && !sah.c4.empty();
+    const size_t o_qa = q4 ? L.push(sah.a4.data(), sah.a4.size() * sizeof(float4)) : 0;
+    const size_t o_qb = q4 ? L.push(sah.b4.data(), sah.b4.size() * sizeof(float4)) : 0;
+    const size_t o_qc = q4 ? L.push(sah.c4.data(), sah.c4.size() * sizeof(int4)) : 0;
     WorldConst wcst;
     std::memset(&wcst, 0, sizeof(wcst));
     wcst.cam = w->camera;
@@ -3038,6 +3307,12 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         d.leaf_box = (const float4*)(base + o_lb);
         d.leaf_key = o_lk ? (const uint4*)(base + o_lk) : nullptr;
         d.sah_root = sah.root;
+        if (q4) {
+            d.sah4_a = (const float4*)(base + o_qa);
+            d.sah4_b = (const float4*)(base + o_qb);
+            d.sah4_c = (const int4*)(base + o_qc);
+            d.sah4_root = sah.root4;
+        }
     }
     d.has_light = w->has_light;
     d.wc = (const WorldConst*)(base + o_wc);
@@ -3053,6 +3328,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->depth = std::max(1, depth);
     if (sah.ok) {
         g->sah_nodes = (int32_t)sah.a.size();
+        g->sah4_nodes = (int32_t)sah.c4.size();
         g->depth = std::max(g->depth, sah.depth);
     }
     g->tri_count = w->triangle_count;
@@ -3102,6 +3378,104 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         return rtw::fail(RTW_ERR_OUT_OF_MEMORY, std::string("hipMalloc: ") + hipGetErrorString(e));
     }
     *out = g;
+    return RTW_OK;
+}
+
+// Debug (tools/ only, not part of include/rtw.h): the SAH tree build_sah_tables makes for a world --
+// out[0] nodes, out[1] depth, out[2] expected node tests and out[3] expected leaf tests per ray by the
+// surface-area measure (each node's and leaf reference's box area over the root's), out[4] 1 if the
+// world qualifies for the SAH path.  No GPU needed.
+extern "C" RTW_API int rtw_debug_sah_tree(const rtw_world* w, double* out) {
+    if (!w || !out) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    const SahTables S = build_sah_tables(w);
+    for (int i = 0; i < 10; ++i) out[i] = 0.0;
+    out[4] = S.ok ? 1.0 : 0.0;
+    if (!S.ok) return RTW_OK;
+    auto area = [](float4 a, float4 b) {
+        const double dx = (double)a.w - a.x, dy = (double)b.x - a.y, dz = (double)b.y - a.z;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    // measured over the subtree of the root's internal child when the other child is a leaf (suzanne's
+    // ground sphere would otherwise make every mesh node's area vanish against the root's)
+    int32_t root = S.root;
+    if (root >= 0) {
+        const int32_t l = (int32_t)fbits(S.b[(size_t)root].z) >> 2, r = (int32_t)fbits(S.b[(size_t)root].w);
+        if ((l < 0) != (r < 0)) root = l >= 0 ? l : r;
+    }
+    double nodes = 1.0, leaves = 0.0;  // the top node's test; a child is tested when its parent passes
+    if (root >= 0) {
+        const double ar = area(S.a[(size_t)root], S.b[(size_t)root]);
+        std::vector<int32_t> todo{root};
+        while (!todo.empty()) {
+            const int32_t i = todo.back();
+            todo.pop_back();
+            const double an = area(S.a[(size_t)i], S.b[(size_t)i]) / ar;
+            for (int c = 0; c < 2; ++c) {
+                const int32_t ch = c ? (int32_t)fbits(S.b[(size_t)i].w) : ((int32_t)fbits(S.b[(size_t)i].z) >> 2);
+                (ch < 0 ? leaves : nodes) += an;
+                if (ch >= 0) todo.push_back(ch);
+            }
+        }
+    }
+    out[0] = (double)S.a.size();
+    out[1] = (double)S.depth;
+    out[2] = nodes;
+    out[3] = leaves;
+    // experiment estimates (out[5..9]): the two-children walk's steps and box tests, and those of the
+    // same tree collapsed to 4 children per node (each child replaced by its children, largest box
+    // first, until 4): steps, box tests, leaf tests, all per ray by the area measure
+    if (root >= 0) {
+        const double ar = area(S.a[(size_t)root], S.b[(size_t)root]);
+        auto kids = [&](int32_t i, int c) { return c ? (int32_t)fbits(S.b[(size_t)i].w) : ((int32_t)fbits(S.b[(size_t)i].z) >> 2); };
+        double st2 = 0.0, bx2 = 0.0, st4 = 0.0, bx4 = 0.0, lf4 = 0.0;
+        std::vector<int32_t> todo{root};
+        while (!todo.empty()) {
+            const int32_t i = todo.back();
+            todo.pop_back();
+            const double an = area(S.a[(size_t)i], S.b[(size_t)i]) / ar;
+            st2 += an;
+            for (int c = 0; c < 2; ++c) {
+                const int32_t ch = kids(i, c);
+                if (ch >= 0) {
+                    bx2 += an;
+                    todo.push_back(ch);
+                }
+            }
+        }
+        std::vector<int32_t> todo4{root};
+        while (!todo4.empty()) {
+            const int32_t i = todo4.back();
+            todo4.pop_back();
+            const double an = area(S.a[(size_t)i], S.b[(size_t)i]) / ar;
+            std::vector<int32_t> ch{kids(i, 0), kids(i, 1)};
+            while (ch.size() < 4) {
+                int best = -1;
+                double ba = -1.0;
+                for (size_t c = 0; c < ch.size(); ++c)
+                    if (ch[c] >= 0 && area(S.a[(size_t)ch[c]], S.b[(size_t)ch[c]]) > ba)
+                        ba = area(S.a[(size_t)ch[c]], S.b[(size_t)ch[c]]), best = (int)c;
+                if (best < 0) break;
+                const int32_t x = ch[(size_t)best];
+                ch.erase(ch.begin() + best);
+                ch.push_back(kids(x, 0));
+                ch.push_back(kids(x, 1));
+            }
+            st4 += an;
+            for (int32_t c : ch) {
+                if (c >= 0) {
+                    bx4 += an;
+                    todo4.push_back(c);
+                } else {
+                    lf4 += an;
+                }
+            }
+        }
+        out[5] = st2;
+        out[6] = bx2;
+        out[7] = st4;
+        out[8] = bx4;
+        out[9] = lf4;
+    }
     return RTW_OK;
 }
 
@@ -3218,12 +3592,6 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         if (e[0] == '0') A.coop_ties = 0;
     if (const char* e = std::getenv("RTW_COOP_AUDIT"))  // tests only: the DFS-last tied leaf
         if (e[0] == '1' && A.coop_ties) A.coop_ties = 2;
-    A.node_count = sah ? g->sah_nodes : g->node_count;
-    const size_t scene_bytes =
-        (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
-    const size_t tri_bytes = (size_t)4 * RTW_TRI_SOA * sizeof(float4);  // mode 2: component-major, fixed stride
-    const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
-    const size_t stack16_bytes = stack_bytes / 2;  // mode 2: 16-bit entries
     // a block may take its share of the CU's LDS at the kernel's target occupancy
     // (RTW_MIN_WAVES_PER_SIMD waves on each of 4 SIMDs)
     const int blocks_per_cu = std::max(1, (4 * RTW_MIN_WAVES_PER_SIMD * 64) / RTW_BLOCK);
@@ -3231,12 +3599,29 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
 #ifdef RTW_PHASE_TIMING
     cap -= (RTW_BLOCK / 64) * 10 * sizeof(unsigned long long);  // the per-wave phase sums (pt_slot)
 #endif
+    const size_t tri_bytes = (size_t)4 * RTW_TRI_SOA * sizeof(float4);  // mode 2: component-major, fixed stride
+    const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
+    const size_t stack16_bytes = stack_bytes / 2;  // mode 2: 16-bit entries
+    const char* lds_mode_env = std::getenv("RTW_LDS_MODE");  // audits: cap the mode
+    // the 4-wide walk (traverse4) where its tree exists (plain-sphere worlds) and fits in LDS (mode 1)
+    bool sah4 = sah && lk == LK_SPHERES && g->sah4_nodes > 0;
+    if (sah4 && ((size_t)(9 * g->sah4_nodes + g->leaf_count) * sizeof(float4) + stack_bytes > cap ||
+                 (lds_mode_env && std::atoi(lds_mode_env) < 1)))
+        sah4 = false;
+    A.sah4 = sah4 ? 1 : 0;
+    A.node_count = sah4 ? g->sah4_nodes : sah ? g->sah_nodes : g->node_count;
+    // LDS scene: 4-wide [a 4n][b 4n][children n][leaf records L], else [node_a n][node_b n][leaf records L]
+    // [cull constants (n + 1) / 2][rects 2R] (+ the triangle records in mode 2)
+    const size_t scene_bytes =
+        sah4 ? (size_t)(9 * A.node_count + g->leaf_count) * sizeof(float4)
+             : (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
+    A.fast_off = sah4 ? 9 * A.node_count : 2 * A.node_count;
     int mode = 0;
-    if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 && A.node_count < 32768 && g->node_count < 32768 &&
-        scene_bytes + tri_bytes + stack16_bytes <= cap)
+    if (!sah4 && g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 && A.node_count < 32768 &&
+        g->node_count < 32768 && scene_bytes + tri_bytes + stack16_bytes <= cap)
         mode = 2;
     else if (scene_bytes + stack_bytes <= cap) mode = 1;
-    if (const char* e = std::getenv("RTW_LDS_MODE")) mode = std::min(mode, std::atoi(e));  // audits: cap the mode
+    if (lds_mode_env) mode = std::min(mode, std::atoi(lds_mode_env));
     size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes + stack16_bytes : stack_bytes);
     // shading tables after the scene when they fit too (RTW_NO_SHADE_LDS=1: keep them in HBM / L2)
     const int32_t scene_f4 = (int32_t)((scene_bytes + (mode == 2 ? tri_bytes : 0)) / sizeof(float4));
@@ -3267,7 +3652,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         g->last_kernel[0] = mode;
         g->last_kernel[1] = lk;
         g->last_kernel[2] = tx;
-        g->last_kernel[3] = sah ? 1 : 0;
+        g->last_kernel[3] = sah4 ? 2 : sah ? 1 : 0;  // 2: the 4-wide SAH walk
     }
     const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -3318,7 +3703,7 @@ uint64_t queue_cap(uint64_t items) {
 void set_items(KArgs& A, uint32_t chunk) {
     const uint32_t n = A.s_end - A.s_begin;
     // chunk-major order drains on single-sample items; in cost order the cheapest tiles come last
-    const uint32_t tail = A.tile_perm ? 0u : std::min<uint32_t>(n, (uint32_t)env_size("RTW_TAIL_SAMPLES", 8));
+    const uint32_t tail = A.tile_perm || A.whole_pixel ? 0u : std::min<uint32_t>(n, (uint32_t)env_size("RTW_TAIL_SAMPLES", 8));
     A.chunk = chunk;
     A.s_split = A.s_end - tail;
     A.items_big = (uint64_t)A.total * ((A.s_split - A.s_begin + chunk - 1) / chunk);
@@ -3372,7 +3757,11 @@ int render_frame(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t
 int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream,
                       std::vector<uint64_t>* launch_items) {
     if (A.total == 0) return RTW_OK;
-    const uint32_t chunk = (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 1));
+    // Whole-pixel items (KArgs::whole_pixel): thread_count 1 only (the planes' merge needs every
+    // plane's value), never in the counting variant; RTW_WHOLE_PIXEL=1 selects them (A/B runs)
+    A.whole_pixel = 0;
+    if (!stats && A.thread_count <= 1 && env_size("RTW_WHOLE_PIXEL", 0) == 1) A.whole_pixel = 1;
+    const uint32_t chunk = A.whole_pixel ? A.spp : (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 1));
     // The colour buffer sets the launches per frame (C5, 4K x 2048 spp = 204 GB of colours: 13
     // launches at a fixed 16 GiB, 4 at 64 GiB, one per rank of an 8-GPU split).  Default: half of
     // the HBM this world could use (free memory plus the buffer it already holds), at most 64 GiB.
@@ -3400,7 +3789,8 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
     // come out of the budget first.  One launch merges straight from the colours (no plane buffer).
     const bool plane_buffer = n_planes > 1 && per_launch < A.spp;
     if (plane_buffer) per_launch = launch_samples(budget > per_sample * n_planes ? budget - per_sample * n_planes : 0);
-    int rc = grow((void**)&g->colors, &g->colors_bytes, per_sample * per_launch);
+    if (A.whole_pixel) per_launch = A.spp;  // one launch, no colour buffer
+    int rc = A.whole_pixel ? RTW_OK : grow((void**)&g->colors, &g->colors_bytes, per_sample * per_launch);
     if (rc != RTW_OK) return rc;
     if (plane_buffer) {
         rc = grow((void**)&g->running, &g->running_bytes, per_sample * n_planes);
@@ -3465,7 +3855,9 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
         rc = launch_render(g, A, stats ? LK_STATS : LK_RENDER, stream);
         if (rc != RTW_OK) return rc;
         const unsigned blocks = (A.total + 255) / 256;
-        if (n_planes > 1 && !plane_buffer)
+        if (A.whole_pixel) {
+            // the render kernel wrote the pixels
+        } else if (n_planes > 1 && !plane_buffer)
             hipLaunchKernelGGL(merge_planes_direct_kernel, dim3(blocks), dim3(256), 0, stream, (const float*)g->colors,
                                A.total, n_planes, whole, rem, out, A.layout, A.width, A.height, A.tile_w, A.tile_h,
                                A.tiles_x, A.part_index, A.part_count);

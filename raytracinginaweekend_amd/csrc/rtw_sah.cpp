@@ -120,9 +120,313 @@ int32_t build(Item* it, size_t n, std::vector<rtw_bvh_node>& nodes, int depth, i
     return id;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Spatial splits (Stich, Friedrich & Dietrich 2009, "Spatial splits in bounding volume
+// hierarchies"): a node may split space at a plane instead of splitting its references by centre; a
+// triangle straddling the plane is then referenced on both sides, each reference with the box of its
+// part (the triangle clipped to the side, exactly, in double, rounded outward to f32).  The union of
+// a leaf's reference boxes covers the leaf, so a walk with the proximity cull still tests, somewhere,
+// every leaf whose test would accept a root; a leaf met twice reports the same t.
+// Non-triangle references straddling a plane are clipped as boxes (their box cut by the plane).
+// ---------------------------------------------------------------------------------------------
+// f32 box outward from a double box: below 2^-60 in magnitude a bound snaps outward to 0 or +-2^-60
+// (every SAH box coordinate stays 0 or >= 2^-60, as the upload checks)
+void round_out(const double lo[3], const double hi[3], float flo[3], float fhi[3]) {
+    const double tiny = 0x1p-60;
+    for (int k = 0; k < 3; ++k) {
+        double l = lo[k] - std::fabs(lo[k]) * 0x1p-45, h = hi[k] + std::fabs(hi[k]) * 0x1p-45;
+        if (std::fabs(l) < tiny) l = l < 0.0 ? -tiny : 0.0;
+        if (std::fabs(h) < tiny) h = h > 0.0 ? tiny : 0.0;
+        float a = (float)l, b = (float)h;
+        if ((double)a > l) a = std::nextafter(a, -INFINITY);
+        if ((double)b < h) b = std::nextafter(b, INFINITY);
+        flo[k] = a;
+        fhi[k] = b;
+    }
+}
+
+struct Ref {
+    double lo[3], hi[3];  // the reference's box (exact clip results; rounded outward at the end)
+    int32_t leaf;         // leaf index
+};
+
+struct SplitBuilder {
+    const float* tri;  // 9 floats per leaf (the triangle's vertices), x = NaN: not a clippable triangle
+    const float* lkm;  // per leaf {k, m} proximity-cull constants; k < 0: a leaf that never reports a hit
+    int64_t extra;     // references still allowed beyond one per leaf
+    std::vector<rtw_bvh_node>* nodes;
+    std::vector<float>* km;  // 2 per node: the maxima over the leaves below
+    int max_depth = 0;
+    struct Out {
+        int32_t id;
+        float lo[3], hi[3];
+        float k, m;
+    };
+
+    static double area(const double lo[3], const double hi[3]) {
+        const double dx = std::max(0.0, hi[0] - lo[0]), dy = std::max(0.0, hi[1] - lo[1]), dz = std::max(0.0, hi[2] - lo[2]);
+        return dx * dy + dy * dz + dz * dx;
+    }
+    // the box of (the reference's leaf) within [lo, hi] (a sub-box of the reference's box)
+    void clip(const Ref& r, const double lo[3], const double hi[3], double olo[3], double ohi[3]) const {
+        const float* t = tri ? tri + 9 * (size_t)r.leaf : nullptr;
+        if (!t || t[0] != t[0]) {  // a box: cut it
+            for (int k = 0; k < 3; ++k) {
+                olo[k] = std::max(r.lo[k], lo[k]);
+                ohi[k] = std::min(r.hi[k], hi[k]);
+            }
+            return;
+        }
+        // Sutherland-Hodgman against the six planes of [lo, hi]
+        double poly[2][16][3];
+        int n = 3, cur = 0;
+        for (int v = 0; v < 3; ++v)
+            for (int k = 0; k < 3; ++k) poly[0][v][k] = t[3 * v + k];
+        for (int k = 0; k < 3 && n > 0; ++k)
+            for (int side = 0; side < 2 && n > 0; ++side) {
+                const double c = side ? hi[k] : lo[k];
+                auto inside = [&](const double* p) { return side ? p[k] <= c : p[k] >= c; };
+                int m = 0;
+                for (int v = 0; v < n; ++v) {
+                    const double* p = poly[cur][v];
+                    const double* q = poly[cur][(v + 1) % n];
+                    const bool pi = inside(p), qi = inside(q);
+                    if (pi) {
+                        for (int j = 0; j < 3; ++j) poly[cur ^ 1][m][j] = p[j];
+                        ++m;
+                    }
+                    if (pi != qi) {
+                        const double f = (c - p[k]) / (q[k] - p[k]);
+                        for (int j = 0; j < 3; ++j) poly[cur ^ 1][m][j] = p[j] + f * (q[j] - p[j]);
+                        poly[cur ^ 1][m][k] = c;
+                        ++m;
+                    }
+                }
+                n = m;
+                cur ^= 1;
+            }
+        for (int k = 0; k < 3; ++k) {
+            olo[k] = INFINITY;
+            ohi[k] = -INFINITY;
+        }
+        for (int v = 0; v < n; ++v)
+            for (int k = 0; k < 3; ++k) {
+                olo[k] = std::min(olo[k], poly[cur][v][k]);
+                ohi[k] = std::max(ohi[k], poly[cur][v][k]);
+            }
+        for (int k = 0; k < 3; ++k) {  // inside the clip box and the reference's box (rounding in the clip)
+            olo[k] = std::max(olo[k], std::max(lo[k], r.lo[k]));
+            ohi[k] = std::min(ohi[k], std::min(hi[k], r.hi[k]));
+        }
+    }
+
+    Out build(std::vector<Ref>& refs, int depth) {
+        max_depth = std::max(max_depth, depth);
+        const size_t n = refs.size();
+        if (n == 1) {
+            Out o;
+            o.id = -1 - refs[0].leaf;
+            round_out(refs[0].lo, refs[0].hi, o.lo, o.hi);
+            const float k = lkm[2 * (size_t)refs[0].leaf], m = lkm[2 * (size_t)refs[0].leaf + 1];
+            o.k = k < 0.0f ? 0.0f : k;  // a leaf that never reports a hit constrains nothing
+            o.m = k < 0.0f ? 0.0f : m;
+            return o;
+        }
+        double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (const Ref& r : refs)
+            for (int k = 0; k < 3; ++k) {
+                blo[k] = std::min(blo[k], r.lo[k]);
+                bhi[k] = std::max(bhi[k], r.hi[k]);
+                const double c = 0.5 * (r.lo[k] + r.hi[k]);
+                clo[k] = std::min(clo[k], c);
+                chi[k] = std::max(chi[k], c);
+            }
+        // object split: binned SAH over the centres
+        double best = INFINITY;
+        int axis = -1, best_bin = -1;
+        if (depth < kSahDepth)
+            for (int k = 0; k < 3; ++k) {
+                const double ext = chi[k] - clo[k];
+                if (!(ext > 0.0)) continue;
+                double bl[kBins][3], bh[kBins][3];
+                size_t cnt[kBins] = {};
+                for (int b = 0; b < kBins; ++b)
+                    for (int j = 0; j < 3; ++j) bl[b][j] = INFINITY, bh[b][j] = -INFINITY;
+                for (const Ref& r : refs) {
+                    const int b = std::min(kBins - 1, std::max(0, (int)((0.5 * (r.lo[k] + r.hi[k]) - clo[k]) / ext * kBins)));
+                    ++cnt[b];
+                    for (int j = 0; j < 3; ++j) bl[b][j] = std::min(bl[b][j], r.lo[j]), bh[b][j] = std::max(bh[b][j], r.hi[j]);
+                }
+                double rc[kBins] = {}, al[3] = {INFINITY, INFINITY, INFINITY}, ah[3] = {-INFINITY, -INFINITY, -INFINITY};
+                size_t rn = 0;
+                for (int b = kBins - 1; b >= 1; --b) {
+                    for (int j = 0; j < 3; ++j) al[j] = std::min(al[j], bl[b][j]), ah[j] = std::max(ah[j], bh[b][j]);
+                    rn += cnt[b];
+                    rc[b] = rn ? area(al, ah) * (double)rn : 0.0;
+                }
+                double ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+                size_t ln = 0;
+                for (int b = 0; b < kBins - 1; ++b) {
+                    for (int j = 0; j < 3; ++j) ll[j] = std::min(ll[j], bl[b][j]), lh[j] = std::max(lh[j], bh[b][j]);
+                    ln += cnt[b];
+                    if (ln == 0 || ln == n) continue;
+                    const double c = area(ll, lh) * (double)ln + rc[b + 1];
+                    if (c < best) best = c, axis = k, best_bin = b;
+                }
+            }
+        // spatial split: bins over the node box; a reference counts on every side it reaches
+        double sbest = INFINITY, splane = 0.0;
+        int saxis = -1;
+        if (depth < kSahDepth && extra > 0)
+            for (int k = 0; k < 3; ++k) {
+                const double ext = bhi[k] - blo[k];
+                if (!(ext > 0.0)) continue;
+                double bl[kBins][3], bh[kBins][3];
+                size_t enter[kBins] = {}, leave[kBins] = {};
+                for (int b = 0; b < kBins; ++b)
+                    for (int j = 0; j < 3; ++j) bl[b][j] = INFINITY, bh[b][j] = -INFINITY;
+                auto pos = [&](int b) { return b == kBins ? bhi[k] : blo[k] + ext * b / kBins; };
+                for (const Ref& r : refs) {
+                    const int b0 = std::min(kBins - 1, std::max(0, (int)((r.lo[k] - blo[k]) / ext * kBins)));
+                    const int b1 = std::min(kBins - 1, std::max(b0, (int)((r.hi[k] - blo[k]) / ext * kBins)));
+                    ++enter[b0];
+                    ++leave[b1];
+                    for (int b = b0; b <= b1; ++b) {
+                        double lo[3] = {blo[0], blo[1], blo[2]}, hi[3] = {bhi[0], bhi[1], bhi[2]}, ol[3], oh[3];
+                        lo[k] = pos(b);
+                        hi[k] = pos(b + 1);
+                        if (b0 == b1) {
+                            for (int j = 0; j < 3; ++j) ol[j] = r.lo[j], oh[j] = r.hi[j];
+                        } else {
+                            clip(r, lo, hi, ol, oh);
+                        }
+                        for (int j = 0; j < 3; ++j) bl[b][j] = std::min(bl[b][j], ol[j]), bh[b][j] = std::max(bh[b][j], oh[j]);
+                    }
+                }
+                double rc[kBins] = {}, al[3] = {INFINITY, INFINITY, INFINITY}, ah[3] = {-INFINITY, -INFINITY, -INFINITY};
+                size_t rn = 0;
+                for (int b = kBins - 1; b >= 1; --b) {
+                    for (int j = 0; j < 3; ++j) al[j] = std::min(al[j], bl[b][j]), ah[j] = std::max(ah[j], bh[b][j]);
+                    rn += leave[b];
+                    rc[b] = rn ? area(al, ah) * (double)rn : 0.0;
+                }
+                double ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+                size_t ln = 0, rn2 = n;
+                for (int b = 0; b < kBins - 1; ++b) {
+                    for (int j = 0; j < 3; ++j) ll[j] = std::min(ll[j], bl[b][j]), lh[j] = std::max(lh[j], bh[b][j]);
+                    ln += enter[b];
+                    rn2 -= leave[b];
+                    if (ln == 0 || rn2 == 0 || ln == n || rn2 == n || (int64_t)(ln + rn2 - n) > extra) continue;
+                    const double c = area(ll, lh) * (double)ln + rc[b + 1];
+                    if (c < sbest) sbest = c, saxis = k, splane = pos(b + 1);
+                }
+            }
+        std::vector<Ref> left, right;
+        if (saxis >= 0 && sbest < best) {
+            for (const Ref& r : refs) {
+                if (r.hi[saxis] <= splane) {
+                    left.push_back(r);
+                } else if (r.lo[saxis] >= splane) {
+                    right.push_back(r);
+                } else {
+                    Ref a = r, b = r;
+                    double lo[3] = {r.lo[0], r.lo[1], r.lo[2]}, hi[3] = {r.hi[0], r.hi[1], r.hi[2]};
+                    hi[saxis] = splane;
+                    clip(r, lo, hi, a.lo, a.hi);
+                    lo[saxis] = splane;
+                    hi[saxis] = r.hi[saxis];
+                    clip(r, lo, hi, b.lo, b.hi);
+                    left.push_back(a);
+                    right.push_back(b);
+                }
+            }
+            if (left.empty() || right.empty() || left.size() == n || right.size() == n ||
+                (int64_t)(left.size() + right.size() - n) > extra) {
+                left.clear();
+                right.clear();
+            } else {
+                extra -= (int64_t)(left.size() + right.size() - n);
+                axis = saxis;
+            }
+        }
+        if (left.empty()) {
+            if (axis >= 0 && best_bin >= 0) {
+                const double ext = chi[axis] - clo[axis];
+                for (const Ref& r : refs) {
+                    const int b = std::min(kBins - 1, std::max(0, (int)((0.5 * (r.lo[axis] + r.hi[axis]) - clo[axis]) / ext * kBins)));
+                    (b <= best_bin ? left : right).push_back(r);
+                }
+            }
+            if (left.empty() || right.empty()) {  // median split on the widest centre axis
+                left.clear();
+                right.clear();
+                axis = 0;
+                for (int k = 1; k < 3; ++k)
+                    if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+                std::vector<Ref> v = refs;
+                const size_t mid = n / 2;
+                std::nth_element(v.begin(), v.begin() + (long)mid, v.end(), [axis](const Ref& a, const Ref& b) {
+                    return a.lo[axis] + a.hi[axis] < b.lo[axis] + b.hi[axis];
+                });
+                left.assign(v.begin(), v.begin() + (long)mid);
+                right.assign(v.begin() + (long)mid, v.end());
+            }
+        }
+        refs.clear();
+        refs.shrink_to_fit();
+        const int32_t id = (int32_t)nodes->size();
+        nodes->push_back(rtw_bvh_node{});
+        km->push_back(0.0f);
+        km->push_back(0.0f);
+        const Out l = build(left, depth + 1);
+        const Out r = build(right, depth + 1);
+        Out o;
+        o.id = id;
+        rtw_bvh_node& nd = (*nodes)[(size_t)id];
+        for (int k = 0; k < 3; ++k) {
+            o.lo[k] = nd.min[k] = std::min(l.lo[k], r.lo[k]);
+            o.hi[k] = nd.max[k] = std::max(l.hi[k], r.hi[k]);
+        }
+        o.k = std::max(l.k, r.k);
+        o.m = std::max(l.m, r.m);
+        (*km)[2 * (size_t)id] = o.k;
+        (*km)[2 * (size_t)id + 1] = o.m;
+        nd.axis = axis;  // left = the lower side: the near side when ray.d[axis] > 0
+        nd.left = l.id;
+        nd.right = r.id;
+        return o;
+    }
+};
+
 }  // namespace
 
 namespace rtw {
+
+int sah_build_split(const float* lo, const float* hi, const float* tri, const float* leaf_km, int32_t n, double budget,
+                    std::vector<rtw_bvh_node>& nodes, std::vector<float>& km, int32_t* root, int* depth) {
+    nodes.clear();
+    km.clear();
+    if (n <= 1) return -1;
+    std::vector<Ref> refs((size_t)n);
+    for (int32_t i = 0; i < n; ++i) {
+        for (int k = 0; k < 3; ++k) {
+            refs[(size_t)i].lo[k] = lo[3 * (size_t)i + k];
+            refs[(size_t)i].hi[k] = hi[3 * (size_t)i + k];
+        }
+        refs[(size_t)i].leaf = i;
+    }
+    SplitBuilder B;
+    B.tri = tri;
+    B.lkm = leaf_km;
+    B.extra = (int64_t)(budget * n);
+    B.nodes = &nodes;
+    B.km = &km;
+    nodes.reserve((size_t)n + (size_t)B.extra);
+    *root = B.build(refs, 0).id;
+    *depth = B.max_depth;
+    return 0;
+}
 
 int sah_build(const float* lo, const float* hi, int32_t n, std::vector<rtw_bvh_node>& nodes, int32_t* root,
               int* depth) {

@@ -154,7 +154,7 @@ def test_sah_tree_agrees(worlds, name, monkeypatch):
     tree's order, re-traced there where the proof fails) give the reference-tree loop's bits
     (RTW_NO_SAH=1) on a GPU-filling frame, and the oracle's on a small one."""
     world = worlds(name)
-    assert _kernel_tree(world) == "sah"
+    assert _kernel_tree(world).startswith("sah")
     size = R.Size2i(320, 180)
     sah = R.render(size, 1, 8, 50, world, seed=29)
     small = R.render(R.Size2i(40, 24), 1, 4, 50, world, seed=29)
@@ -165,7 +165,7 @@ def test_sah_tree_agrees(worlds, name, monkeypatch):
     assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(40, 24), 4, 50, seed=29)), name)
 
 
-def _tie_world():
+def _tie_world(mesh: bool = True):
     """Exact ties and grazing hits: four coincident spheres with different materials (every hit on
     them is a tie the reference breaks by its DFS order), a row of touching spheres (tangent
     points on shared box planes), and a quad of two triangles twice over (coincident triangles,
@@ -186,8 +186,9 @@ def _tie_world():
         return list(p[a]) + list(p[b]) + list(p[c]) + list(n) * 3 + [0.0] * 6
 
     quad = np.array([tri(0, 1, 2), tri(0, 2, 3)], np.float32)
-    g.add(wb.new_mesh(quad, mats[1]))
-    g.add(wb.new_mesh(quad, mats[2]))
+    if mesh:
+        g.add(wb.new_mesh(quad, mats[1]))
+        g.add(wb.new_mesh(quad, mats[2]))
     cam = R.Camera.build().vertical_fov(40.0, 9.0 / 16.0).position((0.3, 1.2, 5.0)).look_at((0, 1, 0), (0, 0.5, 0)).build()
     return g.build().finish(wb, R.BackgroundColor.sky(), cam)
 
@@ -217,7 +218,7 @@ def _tie_world_wrapped():
 
 def test_sah_wrapped_ties_and_grazing_hits(monkeypatch):
     world = _tie_world_wrapped()
-    assert _kernel_tree(world) == "sah"
+    assert _kernel_tree(world).startswith("sah")
     size = R.Size2i(96, 54)
     gpu = R.render(size, 1, 8, 50, world, seed=37)
     assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=37)), "wrapped tie world")
@@ -252,7 +253,7 @@ def test_sah_rolling_shutter_motion(pace, monkeypatch):
     shutter's included (rtw_cull.h rtw_ray_time_range): bit-exact against the oracle and the
     reference-tree loop with a non-zero shutter_pace."""
     world = _rolling_shutter_world(pace)
-    assert _kernel_tree(world) == "sah"
+    assert _kernel_tree(world).startswith("sah")
     size = R.Size2i(96, 54)
     gpu = R.render(size, 1, 8, 50, world, seed=43)
     assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=43)), f"rolling shutter {pace}")
@@ -264,7 +265,7 @@ def test_sah_rolling_shutter_motion(pace, monkeypatch):
 
 def test_sah_ties_and_grazing_hits(monkeypatch):
     world = _tie_world()
-    assert _kernel_tree(world) == "sah"
+    assert _kernel_tree(world).startswith("sah")
     size = R.Size2i(96, 54)
     gpu = R.render(size, 1, 8, 50, world, seed=31)
     assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=31)), "tie world")
@@ -281,7 +282,7 @@ def test_coop_tie_resolution_decides_images(monkeypatch):
     setting that keeps the DFS-last tied leaf changes the image (the resolution decides pixels)."""
     world = _tie_world()
     dw = R.DeviceWorld(world, 0)
-    assert _kernel_tree(world) == "sah"
+    assert _kernel_tree(world).startswith("sah")
     import torch
 
     out = torch.empty(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
@@ -404,3 +405,49 @@ def test_one_world_two_streams_bit_exact(worlds):
     torch.cuda.synchronize()
     assert_bit_identical(a.cpu().numpy().reshape(-1, 3), O.render(world, p1), "stream 1")
     assert_bit_identical(b.cpu().numpy().reshape(-1, 3), O.render(world, p2), "stream 2")
+
+
+@pytest.mark.parametrize("name,parts", [("final_scene1", 1), ("earth_motion", 1), ("suzanne", 1), ("final_scene1", 3)])
+def test_whole_pixel_items_bit_exact(worlds, name, parts, monkeypatch):
+    """Whole-pixel work items (RTW_WHOLE_PIXEL=1: one lane renders all of a pixel's samples in order and
+    sums them in registers, no colour buffer): the oracle's bits, in image layout and as tile partitions,
+    over a chunk-major first frame and cost-ordered later frames."""
+    import torch
+
+    from raytracinginaweekend_amd.distributed import FrameRenderer, FrameSpec, untile_host
+
+    monkeypatch.setenv("RTW_WHOLE_PIXEL", "1")
+    world = worlds(name)
+    size = R.Size2i(72, 40)
+    spec = FrameSpec(size, 9, 50, 7)
+    ref = O.render(world, R.render_params(size, 9, 50, seed=7))
+    bufs = []
+    for rank in range(parts):
+        fr = FrameRenderer(world, spec, rank, parts, 0)
+        for _ in range(2):
+            fr.launch()
+            torch.cuda.synchronize()
+            bufs_r = (fr.image if parts == 1 else fr.tiles).cpu().numpy().copy()
+            if parts == 1:
+                assert_bit_identical(bufs_r.reshape(-1, 3), ref, f"{name} whole-pixel items")
+        bufs.append(bufs_r)
+    if parts > 1:
+        img = untile_host(np.concatenate(bufs), size, spec.tile, parts, len(bufs[0]))
+        assert_bit_identical(img, ref, f"{name} whole-pixel items, {parts} partitions")
+
+
+@pytest.mark.parametrize("name", ["final_scene1", "defocus_blur", "simple_plane", "spheres_ties"])
+def test_sah4_walk_agrees(worlds, name, monkeypatch):
+    """the 4-wide SAH walk of plain-sphere worlds gives the two-children walk's bits
+    (RTW_SAH4=0) on a GPU-filling frame -- ties and grazing hits included (coincident and touching
+    spheres) -- and the oracle's on a small one."""
+    world = _tie_world(mesh=False) if name == "spheres_ties" else worlds(name)
+    monkeypatch.setenv("RTW_SAH4", "1")
+    assert _kernel_tree(world) == "sah4"
+    size = R.Size2i(320, 180)
+    four = R.render(size, 1, 8, 50, world, seed=47)
+    small = R.render(R.Size2i(48, 27), 1, 6, 50, world, seed=47)
+    assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(48, 27), 6, 50, seed=47)), name)
+    monkeypatch.setenv("RTW_SAH4", "0")
+    assert _kernel_tree(world) == "sah"
+    assert_bit_identical(four, R.render(size, 1, 8, 50, world, seed=47), name + " 4-wide vs two-children walk")
