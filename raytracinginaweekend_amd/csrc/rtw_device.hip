@@ -384,16 +384,16 @@ __device__ __noinline__ float d_sinf(float x) { return rtw_sinf(x); }
 // sign of the product is read: when rtw_sin_sign_fast decides all three sines' signs (rtw_scalar.h,
 // pinned against glibc's sinf for every f32), the product is negative iff an odd number of them
 // are.  Other arguments (0, huge, NaN, near a multiple of pi/2) evaluate the sines.
-__device__ __noinline__ bool d_checker_odd(float x, float y, float z) {
-    const float c[3] = {x, y, z};
-    bool fast = true, odd = false;
-    for (int i = 0; i < 3; ++i) {
-        int neg;
-        fast = rtw_sin_sign_fast(c[i], &neg) && fast;
-        odd ^= neg != 0;
-    }
-    if (fast) return odd;
-    return d_sinf(x) * d_sinf(y) * d_sinf(z) < 0.0f;
+// the slow path: the three sines inlined in one leaf call (three calls to d_sinf from here kept x, y, z
+// and the product live across calls: 16 B of scratch per lane in every texture variant)
+__device__ __noinline__ bool d_sin3_negative(float x, float y, float z) {
+    return rtw_sinf(x) * rtw_sinf(y) * rtw_sinf(z) < 0.0f;
+}
+__device__ __forceinline__ bool d_checker_odd(float x, float y, float z) {
+    int nx = 0, ny = 0, nz = 0;
+    const bool fast = rtw_sin_sign_fast(x, &nx) & rtw_sin_sign_fast(y, &ny) & rtw_sin_sign_fast(z, &nz);
+    if (__builtin_expect(fast, 1)) return ((nx != 0) ^ (ny != 0) ^ (nz != 0)) != 0;
+    return d_sin3_negative(x, y, z);
 }
 
 struct Ray {
@@ -605,13 +605,25 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
 #else
 #define RTW_TDIV(a, b) ((a) / (b))
 #endif
+// t = num / denom without the division sequence (RTW_TRI_T_MK): with 1e-4 < |denom| <= |d||n| ~ 1 the
+// divisor is inside Markstein's guard; a dividend outside its guard is 0 or below 2^-80
+// (then both quotients lie below ts = 0.001: the test fails either way) -- the upper bound holds as
+// coordinates are below 2^30.  So the quotient decides contains(ts, te, t) as RN(num / denom) does and
+// equals it whenever that passes: no guard, no branch (rtw_device_check_division test 5).
+#ifndef RTW_TRI_T_MK
+#define RTW_TRI_T_MK 0
+#endif
+__device__ __forceinline__ float tri_t_mk(float num, float denom) { return mk_corr(num, denom, rcp_nr(denom)); }
 __device__ __forceinline__ bool tri_test(const TriFast& T, const Ray& r, float ts, float te, float& t) {
     const float denom = dot(r.d, T.n);
     if (!(__builtin_fabsf(denom) > 0.0001f)) return false;
-    // t keeps the IEEE division: its divisor is ray-dependent, and rcp_nr + the correction + the
-    // dividend guard cost suzanne 3 % against it (register pressure in the leaf body;
-    // profiles/r03/v5_division_ab.txt)
+    // t keeps the IEEE division unless RTW_TRI_T_MK: rcp_nr + the correction + a dividend guard cost
+    // suzanne 3 % against it (register pressure in the leaf body; profiles/r03/v5_division_ab.txt)
+#if RTW_TRI_T_MK && !defined(RTW_EXP_FASTDIV_TRI)
+    t = tri_t_mk(dot(sub(T.p0, r.o), T.n), denom);
+#else
     t = RTW_TDIV(dot(sub(T.p0, r.o), T.n), denom);
+#endif
     if (!contains(ts, te, t)) return false;
     const V3 q = sub(at(r, t), T.p0);
 #ifdef RTW_EXP_FASTDIV_TRI
@@ -2615,6 +2627,7 @@ __global__ void eval_node_pass_kernel(const float* box, const float* ray, const 
 //   test 4: a = bits(base + i): sqrt_x (and sqrt_nr inside its range) against sqrtf
 //   test 3: a random pair of any kind (zeros, subnormals, extremes, inf, NaN): div_x, div_tri (y as
 //           tri_prepare sets it), rcp_x and divs_x's components against IEEE division
+//   test 5: tri_t_mk (the triangle's t without a guard) decides contains(0.001, .., t) as a / b does
 // out[0] += mismatches, out[1] = min over mismatching i (the first one, ~0 if none)
 __device__ __forceinline__ uint64_t chk_mix(uint64_t x) {
     x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 27; x *= 0x94D049BB133111EBull; return x ^ (x >> 31);
@@ -2658,6 +2671,19 @@ __global__ void check_division_kernel(int test, uint64_t base, uint64_t n, uint6
             const uint64_t r1 = chk_mix(seed ^ (2 * i)), r2 = chk_mix(seed ^ (2 * i + 1));
             const float a = chk_float(r1, -80, 80), b = chk_float(r2, -22, 22);
             ok = chk_same(mk_corr(a, b, rcp_nr(b)), a / b);
+        } else if (test == 5) {
+            // tri_t_mk: a dividend of any kind (zeros, subnormals, NaN, up to 2^40 in magnitude: num is a
+            // dot product of coordinates below 2^30 with a unit normal), a divisor
+            // with 1e-4 < |b| <= 1.01 (tri_test's range): equal to a / b whenever that is >= 0.001, and
+            // below 0.001 (or NaN alike) whenever a / b is
+            const uint64_t r1 = chk_mix(seed ^ (2 * i)), r2 = chk_mix(seed ^ (2 * i + 1));
+            float a = chk_any(r1);
+            if (((r1 >> 60) & 3) == 0) a = chk_float(r1, -150 + 23, -60);  // tiny dividends
+            if (__builtin_fabsf(a) > 0x1p40f) a = __builtin_copysignf(0x1p40f, a);
+            float b = chk_float(r2, -14, 0);
+            if (__builtin_fabsf(b) <= 1e-4f) b = __builtin_copysignf(1.5e-4f, b);
+            const float q = tri_t_mk(a, b), e = a / b;
+            ok = e >= 0.001f ? chk_same(q, e) : !(q >= 0.001f);
         } else {
             const uint64_t r1 = chk_mix(seed ^ (2 * i)), r2 = chk_mix(seed ^ (2 * i + 1));
             const float a = chk_any(r1), b = chk_any(r2);
@@ -4149,7 +4175,7 @@ extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, c
 
 extern "C" RTW_API int rtw_device_check_division(int device, int test, uint64_t base, uint64_t n, uint64_t seed,
                                                  uint64_t* mismatches, uint64_t* first) {
-    if (!mismatches || !first || test < 0 || test > 4) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
+    if (!mismatches || !first || test < 0 || test > 5) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device");
     HIP_TRY(hipSetDevice(device));

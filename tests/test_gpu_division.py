@@ -56,3 +56,11 @@ def test_sqrt_every_f32():
     # sqrt_x on every bit pattern, sqrt_nr (no range handling) on [2^-96, FLT_MAX]
     bad, first = _check(4, 0, 1 << 32)
     assert bad == 0, f"sqrt_x / sqrt_nr differ from sqrtf on {bad} inputs, first bits {first:#010x}"
+
+
+def test_triangle_t_without_guard():
+    """tri_t_mk (the triangle test's t = num / denom by rcp_nr + Markstein, no guard): for
+    divisors in tri_test's range (1e-4 < |denom| <= ~1) and dividends of any kind, equal to IEEE
+    division whenever the quotient reaches ts = 0.001, and below ts whenever IEEE's is."""
+    bad, first = _check(5, 0, 1 << 31, seed=0x7E57)
+    assert bad == 0, f"{bad} mismatches, first case {first}"

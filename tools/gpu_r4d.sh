@@ -6,9 +6,11 @@ O=gpurun_out/r4d; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 python -c "import bench; print('count_gpus', bench.count_gpus())" > $O/count.txt 2>&1 || exit $?
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
-bash tools/ab_mix.sh "final_scene1" 2 "base|RTW_SAH4=0" "base|" || exit $?
+bash tools/ab_mix.sh "final_scene1" 2 "base|" "base|RTW_SAH4=1" || exit $?
 bash tools/ab_mix.sh "suzanne" 2 "base|" "base|RTW_SAH_SPLIT_BUDGET=0.1" "base|RTW_SAH_SPLIT_BUDGET=0.2" "base|RTW_SAH_SPLIT_BUDGET=0.3" || exit $?
-bash tools/ab_mix.sh "cornell_cube" 1 "base|" "base|RTW_SAH_SPLIT_BUDGET=0.2" || exit $?
+bash tools/ab_mix.sh "cornell_cube" 1 "base|" "base|RTW_SAH_SPLIT_BUDGET=0.2" "tmk|" || exit $?
+bash tools/ab_mix.sh "suzanne" 2 "tmk|" || exit $?
+RTW_LIBRARY=$GRAFT_REPO_ROOT/raytracinginaweekend_amd/librtw_tmk.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q -k "suzanne or cornell or tie" --timeout 200 --timeout-method thread > $O/tmk_tests.log 2>&1 || exit $?
 RTW_SAH_SPLIT_BUDGET=0.2 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "sah or suzanne or cornell or tie" --timeout 200 --timeout-method thread > $O/split_tests.log 2>&1 || exit $?
 B="--no-cpu-baseline --no-stats --no-pmc --no-first-frame --no-thread-count --no-configs"
 for r in 1 2; do
