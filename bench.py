@@ -218,7 +218,7 @@ def configs_pmc(args, legs: list, peak_ginstr: float) -> None:
               "insts_per_frame": int(v["SQ_INSTS_VALU"]),
               "lane_utilisation": round(v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"]), 4),
               "wait_any_frac": round(v["SQ_WAIT_ANY"] / v["SQ_WAVE_CYCLES"], 4),
-              "launches_per_frame": v["launches"]}
+              "pmc_launches_per_frame": v["launches"]}
         write = v.get("WRITE_SIZE", 0.0) * 1024.0
         if f and "FETCH_SIZE" in f:
             fetch = f["FETCH_SIZE"] * 1024.0 * 2.0

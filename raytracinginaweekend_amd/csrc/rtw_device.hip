@@ -78,6 +78,9 @@
 #define RTW_BATCH_SPREAD 8  // a batch is at most 1/(SPREAD x waves) of the launch's remaining items
 #endif
 #define RTW_STACK 32    // per-lane traversal stack (LDS), >= the BVH depth (checked at upload)
+#ifndef RTW_SAH_SPLIT_BUDGET
+#define RTW_SAH_SPLIT_BUDGET 0.2  // spatial splits in the SAH tree of triangle worlds: extra references per leaf
+#endif
 #ifndef RTW_LDS_SCENE_MAX
 #define RTW_COOP_MAX 4       // drain: live lanes at most for the wave-cooperative trace (RTW_COOP_MAX=0: off)
 #define RTW_COOP_LEAVES 4096 // ... in worlds of at most this many leaves
@@ -611,7 +614,7 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
 // coordinates are below 2^30.  So the quotient decides contains(ts, te, t) as RN(num / denom) does and
 // equals it whenever that passes: no guard, no branch (rtw_device_check_division test 5).
 #ifndef RTW_TRI_T_MK
-#define RTW_TRI_T_MK 0
+#define RTW_TRI_T_MK 1  // suzanne +1.4 %, cornell_cube +1.7 % (profiles/r04/v2_experiments_ab.txt)
 #endif
 __device__ __forceinline__ float tri_t_mk(float num, float denom) { return mk_corr(num, denom, rcp_nr(denom)); }
 __device__ __forceinline__ bool tri_test(const TriFast& T, const Ray& r, float ts, float te, float& t) {
@@ -1760,11 +1763,16 @@ __device__ __forceinline__ Trav traverse4(const DWorld* __restrict__ wp, Trav T,
                     v[a] = sw ? vb : va;
                     v[b] = sw ? va : vb;
                 };
-                cx(0, 1);
-                cx(2, 3);
-                cx(0, 2);
-                cx(1, 3);
-                cx(1, 2);
+#ifndef RTW_Q4_SORT
+#define RTW_Q4_SORT 1
+#endif
+                if (RTW_Q4_SORT) {
+                    cx(0, 1);
+                    cx(2, 3);
+                    cx(0, 2);
+                    cx(1, 3);
+                    cx(1, 2);
+                }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     if (k[j] > -F32_INF) stack[(T.sp++) * RTW_BLOCK] = v[j];
@@ -2903,7 +2911,8 @@ SahTables build_sah_tables(const rtw_world* w) {
     std::vector<rtw_bvh_node> nodes;
     // spatial splits (rtw::sah_build_split) in worlds with plain triangles, RTW_SAH_SPLIT_BUDGET extra
     // references per leaf at most (0: the object-split tree)
-    double budget = 0.0;
+    // (default 0.2: suzanne +1.1 %, cornell_cube +0.1 %, profiles/r04/v2_experiments_ab.txt)
+    double budget = RTW_SAH_SPLIT_BUDGET;
     if (const char* e = std::getenv("RTW_SAH_SPLIT_BUDGET")) budget = std::max(0.0, std::atof(e));
     std::vector<float> tri;
     if (budget > 0.0) {
@@ -2922,13 +2931,40 @@ SahTables build_sah_tables(const rtw_world* w) {
     if (budget > 0.0) {
         // node boxes and cull constants come from the builder: a node's box is the union of its
         // references' clipped boxes, k and m the maxima of the leaves' constants below
-        if (rtw::sah_build_split(lo.data(), hi.data(), tri.data(), lkm.data(), L, budget, nodes, S.km, &S.root, &S.depth) != 0 ||
-            S.depth > RTW_STACK)
-            return S;
-        for (const rtw_bvh_node& nd : nodes)
+        std::vector<rtw_bvh_node> split;
+        std::vector<float> skm;
+        int32_t sroot = 0;
+        int sdepth = 0;
+        bool ok = rtw::sah_build_split(lo.data(), hi.data(), tri.data(), lkm.data(), L, budget, split, skm, &sroot, &sdepth) == 0 &&
+                  sdepth <= RTW_STACK;
+        for (const rtw_bvh_node& nd : split)
             for (int k2 = 0; k2 < 3; ++k2)
-                if (!coord_ok(nd.min[k2]) || !coord_ok(nd.max[k2])) return S;
-    } else {
+                if (!coord_ok(nd.min[k2]) || !coord_ok(nd.max[k2])) ok = false;
+        // the extra nodes must not push a mesh world out of LDS mode 2 (its triangle records in LDS;
+        // launch_render's sizing with the plain tree's depth as a floor): else the plain tree
+        if (ok && w->triangle_count <= RTW_TRI_SOA) {
+            int32_t proot = 0;
+            int pdepth = 0;
+            std::vector<rtw_bvh_node> plain;
+            if (rtw::sah_build(lo.data(), hi.data(), L, plain, &proot, &pdepth) == 0) {
+                auto mode2 = [&](size_t n, int depth) {
+                    return (2 * n + (size_t)L + (n + 1) / 2) * 16 + (size_t)4 * RTW_TRI_SOA * 16 +
+                           (size_t)std::max(depth, pdepth) * RTW_BLOCK * 2;
+                };
+                const size_t cap = RTW_LDS_SCENE_MAX;
+                if (mode2(plain.size(), pdepth) <= cap && mode2(split.size(), sdepth) > cap) ok = false;
+            }
+        }
+        if (ok) {
+            nodes.swap(split);
+            S.km.swap(skm);
+            S.root = sroot;
+            S.depth = sdepth;
+        } else {
+            budget = 0.0;
+        }
+    }
+    if (budget <= 0.0) {
         if (rtw::sah_build(lo.data(), hi.data(), L, nodes, &S.root, &S.depth) != 0 || S.depth > RTW_STACK) return S;
         // cull constants of the SAH tree over the leaves' true world boxes (wrapped leaves included)
         rtw_world tw = *w;
@@ -3785,8 +3821,18 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
     if (A.total == 0) return RTW_OK;
     // Whole-pixel items (KArgs::whole_pixel): thread_count 1 only (the planes' merge needs every
     // plane's value), never in the counting variant; RTW_WHOLE_PIXEL=1 selects them (A/B runs)
+    // Whole-pixel items when the frame has many pixels per resident lane (>= RTW_WHOLE_PIXEL_MIN, default
+    // 16): the frame's tail (each lane's last pixel) is then short against the frame, and the colour
+    // buffer's writes and the accumulation pass go away (C5 on one GPU, 32 pixels per lane: +3.6 %,
+    // profiles/r04/v2_experiments_ab.txt).  With few pixels per lane (an 8-GPU share of C5: 4) single-
+    // sample items balance the lanes.  RTW_WHOLE_PIXEL=1 / 0 forces them on / off.
     A.whole_pixel = 0;
-    if (!stats && A.thread_count <= 1 && env_size("RTW_WHOLE_PIXEL", 0) == 1) A.whole_pixel = 1;
+    if (!stats && A.thread_count <= 1) {
+        const uint64_t lanes = (uint64_t)std::max(1, g->cus) * RTW_BLOCK;
+        const char* wp = std::getenv("RTW_WHOLE_PIXEL");
+        if (wp && wp[0] == '1') A.whole_pixel = 1;
+        else if (!(wp && wp[0] == '0') && (uint64_t)A.total >= env_size("RTW_WHOLE_PIXEL_MIN", 16) * lanes) A.whole_pixel = 1;
+    }
     const uint32_t chunk = A.whole_pixel ? A.spp : (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 1));
     // The colour buffer sets the launches per frame (C5, 4K x 2048 spp = 204 GB of colours: 13
     // launches at a fixed 16 GiB, 4 at 64 GiB, one per rank of an 8-GPU split).  Default: half of

@@ -17,8 +17,8 @@ from tests.parity import assert_bit_identical
 pytestmark = pytest.mark.gpu
 
 # name, width, height, spp, tile stride (prime), owned residue: every BASELINE config at its full
-# size and sample count (C2, C4 on one GPU, C3, C5 on one GPU: 3 launches at the default colour
-# buffer of <= 64 GiB)
+# size and sample count (C2, C4 on one GPU, C3, C5 on one GPU: one launch of whole-pixel work items,
+# 32 pixels per resident lane)
 CASES = [
     ("final_scene1", 1920, 1080, 512, 509, 170),
     ("suzanne", 1920, 1080, 512, 1013, 77),
@@ -83,6 +83,7 @@ def test_full_frame_4k_many_launches(worlds, monkeypatch):
     w, h = 3840, 2160
     size = R.Size2i(w, h)
     monkeypatch.setenv("RTW_SAMPLE_BUFFER_BYTES", str(400 * w * h * 12))
+    monkeypatch.setenv("RTW_WHOLE_PIXEL", "0")  # per-sample items (C5 on one GPU takes whole pixels by default)
     for threads in (1, 7):
         gpu = R.render(size, threads, 2048, 50, world, seed=77)
         p = R.render_params(size, 2048, 50, seed=77, part=(11, 2003), thread_count=threads)

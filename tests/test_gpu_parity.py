@@ -436,7 +436,7 @@ def test_whole_pixel_items_bit_exact(worlds, name, parts, monkeypatch):
         assert_bit_identical(img, ref, f"{name} whole-pixel items, {parts} partitions")
 
 
-@pytest.mark.parametrize("name", ["final_scene1", "defocus_blur", "simple_plane", "spheres_ties"])
+@pytest.mark.parametrize("name", ["final_scene1", "defocus_blur", "perlin_spheres", "spheres_ties"])
 def test_sah4_walk_agrees(worlds, name, monkeypatch):
     """the 4-wide SAH walk of plain-sphere worlds gives the two-children walk's bits
     (RTW_SAH4=0) on a GPU-filling frame -- ties and grazing hits included (coincident and touching

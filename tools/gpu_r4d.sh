@@ -6,7 +6,7 @@ O=gpurun_out/r4d; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 python -c "import bench; print('count_gpus', bench.count_gpus())" > $O/count.txt 2>&1 || exit $?
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
-bash tools/ab_mix.sh "final_scene1" 2 "base|" "base|RTW_SAH4=1" || exit $?
+bash tools/ab_mix.sh "final_scene1" 2 "base|" "base|RTW_SAH4=1" "w5|" "w5|RTW_SAH4=1" || exit $?
 bash tools/ab_mix.sh "suzanne" 2 "base|" "base|RTW_SAH_SPLIT_BUDGET=0.1" "base|RTW_SAH_SPLIT_BUDGET=0.2" "base|RTW_SAH_SPLIT_BUDGET=0.3" || exit $?
 bash tools/ab_mix.sh "cornell_cube" 1 "base|" "base|RTW_SAH_SPLIT_BUDGET=0.2" "tmk|" || exit $?
 bash tools/ab_mix.sh "suzanne" 2 "tmk|" || exit $?
@@ -19,4 +19,7 @@ for r in 1 2; do
   done
 done
 s=$(date +%s); timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit $?; e=$(date +%s); echo "bench wall $((e-s)) s" >> $O/count.txt
+for s in final_scene1 earth_motion suzanne; do
+  RTW_SAH4=1 RTW_LIBRARY=$GRAFT_REPO_ROOT/raytracinginaweekend_amd/librtw_pt.so timeout -k 10 120 python tools/phase_timing.py --scene $s --spp 128 >> $O/phase.txt 2>&1 || exit $?
+done
 echo all-done
