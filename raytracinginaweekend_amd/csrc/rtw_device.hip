@@ -123,14 +123,8 @@ struct DWorld {
     // per axis the bits of the ancestors splitting on it}, bit 31 - k for the ancestor at depth k;
     // null when the reference tree is deeper than 32
     const uint4* leaf_key;
-    // the SAH tree collapsed to four children per node (plain-sphere worlds, traverse4): per node 4 child
-    // records {min.xyz, max.x} (a leaf child: its sphere {c, r}), 4 {max.y, max.z, k, m} and the children
-    // {c0..c3} (>= 0 node, -1 - leaf, RTW_Q4_EMPTY none)
-    const float4* sah4_a;
-    const float4* sah4_b;
-    const int4* sah4_c;
-    int32_t sah4_root;
     int32_t sah_root;
+    int32_t sah_root_c2;  // the SAH root's children packed 16 + 16 bits (the two-children walk's lane state)
     int32_t root;
     int32_t has_light;
 };
@@ -222,7 +216,6 @@ struct KArgs {
     // solid-texture worlds, each texture's first record; the stack follows them (stack_off)
     int32_t sh_li, sh_mat, sh_tex0, stack_off;
     int32_t material_count, texture_count;
-    int32_t sah4;             // 1: the SAH walk runs on the 4-wide tree (node_count = its nodes; traverse4)
     int32_t fast_off;         // LDS float4 offset of the leaf records (leaf_fast)
     int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
                               // re-traced on the reference tree where the proof does not hold (§5.6)
@@ -1475,6 +1468,17 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // so the loop has no leaf steps (final_scene1 +3.0 %, profiles/r03/v9_inline_leaf_ab.txt;
     // RTW_C2_INLINE=0 builds keep round 2's leaf-then-node step)
     constexpr bool C2_INLINE = C2 && RTW_C2_INLINE;
+    // ... and carries, instead of the node it stands on, that node's two children packed in 16 bits each
+    // (C2P): they came with the node's box record in its parent's step (nodes_b.zw), and a pushed node
+    // is pushed as its children -- one dependent LDS read less per step (worlds of < 2^15 nodes and
+    // leaves, checked at upload; RTW_C2_PACKED=0 builds read the children from the node)
+#ifndef RTW_C2_PACKED
+#define RTW_C2_PACKED 1
+#endif
+    constexpr bool C2P = C2_INLINE && RTW_C2_PACKED;
+    auto pack2 = [](float4 nb) {  // {.., .., bits(left << 2 | axis), bits(right)} -> left | right << 16
+        return (int32_t)(((uint32_t)(__float_as_int(nb.z) >> 2) & 0xFFFFu) | ((uint32_t)__float_as_int(nb.w) << 16));
+    };
     // the SAH node test's k term: D^2 (two operations; every world gained 0.5 %,
     // profiles/r03/v6_delta_d2_ab.txt); RTW_SAH_DQ builds keep round 2's Dq form
 #ifdef RTW_SAH_DQ
@@ -1585,17 +1589,25 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             }
         }
 #ifndef RTW_SAH_ONE_CHILD
-        if (C2 && T.phase == ACT && T.node >= 0) {
+        if (C2 && T.phase == ACT && (C2P || T.node >= 0)) {
             // SAH walk, two children per step: the lane stands on a node already accepted (the root,
             // or a child accepted by its parent's step) and tests both children's grown boxes at once
             // (leaf children need no box: their own test follows); accepted children are visited
             // near first (a leaf first), the other one pushed.  Any visit order finds the same
             // closest root (§5.5 step 1), so only the work changes.
-            const float2 ch = reinterpret_cast<const float2*>(nodes_b)[2 * T.node + 1];
-            const int32_t left = __float_as_int(ch.x) >> 2, right = __float_as_int(ch.y);
+            int32_t left, right;
+            if (C2P) {
+                left = (int32_t)(int16_t)(T.node & 0xFFFF);
+                right = T.node >> 16;
+            } else {
+                const float2 ch = reinterpret_cast<const float2*>(nodes_b)[2 * T.node + 1];
+                left = __float_as_int(ch.x) >> 2;
+                right = __float_as_int(ch.y);
+            }
             const int32_t il = left >= 0 ? left : 0, ir = right >= 0 ? right : 0;
             float el, er;
             bool pl, pr;
+            int32_t lc = left, rc = right;  // what stands for an accepted child: C2P its children, else itself
             if (C2_INLINE) {
                 // leaf children: their sphere now (never pushed or visited); internal ones: the box
                 pl = pr = false;
@@ -1606,7 +1618,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                     if (sphere_t(fast[-1 - left], T.ray, 0.001f, T.te, t)) take(t, -1 - left);
                 } else {
                     if (STATS) st.c[ST_NODES]++;
-                    pl = node_pass_cons<SAH_DQ>(nodes_a[left], nodes_b[left], nkm[left], T.ray, rp, 0.001f, T.te, el);
+                    const float4 nb = nodes_b[left];
+                    pl = node_pass_cons<SAH_DQ>(nodes_a[left], nb, nkm[left], T.ray, rp, 0.001f, T.te, el);
+                    if (C2P) lc = pack2(nb);
                 }
                 if (right < 0) {
                     if (STATS) st.c[ST_T_SPHERE]++;
@@ -1614,7 +1628,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                     if (sphere_t(fast[-1 - right], T.ray, 0.001f, T.te, t)) take(t, -1 - right);
                 } else {
                     if (STATS) st.c[ST_NODES]++;
-                    pr = node_pass_cons<SAH_DQ>(nodes_a[right], nodes_b[right], nkm[right], T.ray, rp, 0.001f, T.te, er);
+                    const float4 nb = nodes_b[right];
+                    pr = node_pass_cons<SAH_DQ>(nodes_a[right], nb, nkm[right], T.ray, rp, 0.001f, T.te, er);
+                    if (C2P) rc = pack2(nb);
                 }
             } else {
                 const float4 la = nodes_a[il], lb = nodes_b[il], ra = nodes_a[ir], rb = nodes_b[ir];
@@ -1627,10 +1643,10 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             }
             if (pl && pr) {
                 const bool lf = el <= er;
-                stack[(T.sp++) * RTW_BLOCK] = (StackEntry)(lf ? right : left);
-                T.node = lf ? left : right;
+                stack[(T.sp++) * RTW_BLOCK] = (StackEntry)(lf ? rc : lc);
+                T.node = lf ? lc : rc;
             } else if (pl || pr) {
-                T.node = pl ? left : right;
+                T.node = pl ? lc : rc;
             } else {
                 pop();
             }
@@ -1671,125 +1687,6 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         T.n_nodes = st.c[ST_NODES];
         T.n_sph_rect = st.c[ST_T_SPHERE] | (st.c[ST_T_RECT] << 16);
         T.n_box_tri = st.c[ST_T_BOX] | (st.c[ST_T_TRI] << 16);
-    }
-    return T;
-}
-
-// The SAH walk of plain-sphere worlds on the tree collapsed to four children per node:
-// a lane stands on an accepted node (the root, or a child accepted by its parent's step); its step
-// tests the node's leaf children's spheres first (their hits shrink te), then its internal children's
-// grown boxes (node_pass_cons), moves to the accepted child whose grown box the segment enters first
-// and pushes the other accepted ones.  Against the two-children walk it skips the boxes of every
-// other level and runs half the steps (the step's loop, stack and mask work are per step); the node's
-// nine records are loaded at once, none depends on another.  Step 1 of DESIGN 5.5 holds for any tree
-// whose boxes contain their leaves' accepted points (within delta): the closest root and the tie flag
-// are the two-children walk's.
-#define RTW_Q4_EMPTY ((int32_t)0x80000000)
-#ifndef RTW_Q4_UNROLL
-#define RTW_Q4_UNROLL 2
-#endif
-template <bool STATS>
-__device__ __forceinline__ Trav traverse4(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n4,
-                                       int32_t stack_off, unsigned long long* dbg, int32_t coop_exit) {
-    (void)wp;
-    int32_t off_b = 4 * n4, off_c = 8 * n4;
-    asm volatile("" : "+v"(off_b), "+v"(off_c));
-    const float4* qa = smem;
-    const float4* qb = smem + off_b;
-    const int4* qc = reinterpret_cast<const int4*>(smem + off_c);
-    int32_t* stack = reinterpret_cast<int32_t*>(smem + stack_off) + threadIdx.x;
-    auto take = [&](float t, int leaf) {  // as the two-children walk's (traverse, TM_SAH)
-        const bool tie = T.found >= 0 && T.found != leaf && t == __int_as_float(__float_as_int(T.te) - 1);
-        T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
-        T.te = tie ? T.te : __int_as_float(__float_as_int(t) + 1);
-        T.found = tie ? T.found : leaf;
-    };
-    const RayPre rp{T.inv, true};
-    Stats st;
-    if (STATS)
-        for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
-    (void)dbg;
-    for (;;) {
-        const unsigned long long tr = __ballot(T.phase == PH_TRACE);
-        if (tr == 0) break;
-        if ((uint32_t)__popcll(tr) < (uint32_t)trace_min && __ballot(T.phase == PH_SHADE) != 0) break;
-        if ((int32_t)__popcll(tr) <= coop_exit) break;
-#pragma unroll
-        for (int u = 0; u < (STATS ? 1 : RTW_Q4_UNROLL); ++u) {
-            if (T.phase == PH_TRACE) {
-                const int32_t base = 4 * T.node;
-                const int4 ch = qc[T.node];
-                const int32_t c[4] = {ch.x, ch.y, ch.z, ch.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (c[j] < 0 && c[j] != RTW_Q4_EMPTY) {
-                        if (STATS) st.c[ST_T_SPHERE]++;
-                        float t;
-                        if (sphere_t(qa[base + j], T.ray, 0.001f, T.te, t)) take(t, -1 - c[j]);
-                    }
-                }
-                float be = F32_INF;
-                int32_t bn = -1;
-                float e[4];
-                bool acc[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc[j] = false;
-                    e[j] = F32_INF;
-                    if (c[j] >= 0) {
-                        if (STATS) st.c[ST_NODES]++;
-                        const float4 b = qb[base + j];
-                        acc[j] = node_pass_cons<false>(qa[base + j], b, make_float2(b.z, b.w), T.ray, rp, 0.001f, T.te, e[j]);
-                    }
-                    const bool nearer = acc[j] && e[j] < be;
-                    be = nearer ? e[j] : be;
-                    bn = nearer ? c[j] : bn;
-                }
-                // the other accepted children go on the stack, the farthest first (popped last)
-                float k[4];
-                int32_t v[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const bool push = acc[j] && c[j] != bn;
-                    k[j] = push ? e[j] : -F32_INF;
-                    v[j] = c[j];
-                }
-                auto cx = [&](int a, int b) {  // descending by key
-                    const bool sw = k[a] < k[b];
-                    const float ka = k[a], kb = k[b];
-                    const int32_t va = v[a], vb = v[b];
-                    k[a] = sw ? kb : ka;
-                    k[b] = sw ? ka : kb;
-                    v[a] = sw ? vb : va;
-                    v[b] = sw ? va : vb;
-                };
-#ifndef RTW_Q4_SORT
-#define RTW_Q4_SORT 1
-#endif
-                if (RTW_Q4_SORT) {
-                    cx(0, 1);
-                    cx(2, 3);
-                    cx(0, 2);
-                    cx(1, 3);
-                    cx(1, 2);
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (k[j] > -F32_INF) stack[(T.sp++) * RTW_BLOCK] = v[j];
-                if (bn >= 0) {
-                    T.node = bn;
-                } else if (T.sp == 0) {
-                    T.phase = PH_SHADE;
-                } else {
-                    T.node = stack[(--T.sp) * RTW_BLOCK];
-                }
-            }
-        }
-    }
-    if (STATS) {
-        T.n_nodes = st.c[ST_NODES];
-        T.n_sph_rect = st.c[ST_T_SPHERE];
-        T.n_box_tri = 0;
     }
     return T;
 }
@@ -1900,27 +1797,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     // asked for the product kernel's own traversal (stats_tree 1; else the reference's statistics)
     constexpr bool SAHK = LK <= LK_WRAPPED;
     const bool sah = SAHK && A.sah != 0;
-    if (LDS_SCENE && sah && LK == LK_SPHERES && A.sah4) {
-        // the 4-wide tree: [child records a 4n][child records b 4n][children n][leaf records L]
-        const int32_t n4 = A.node_count;
-        for (int i = threadIdx.x; i < 4 * n4; i += RTW_BLOCK) {
-            smem[i] = w.sah4_a[i];
-            smem[4 * n4 + i] = w.sah4_b[i];
-        }
-        for (int i = threadIdx.x; i < n4; i += RTW_BLOCK) reinterpret_cast<int4*>(smem)[8 * n4 + i] = w.sah4_c[i];
-        for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[A.fast_off + i] = w.leaf_fast[i];
-        if (A.sh_li >= 0) {
-            int4* li = reinterpret_cast<int4*>(smem + A.sh_li);
-            for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) li[i] = w.leaf_info[i];
-            int4* mt = reinterpret_cast<int4*>(smem + A.sh_mat);
-            for (int i = threadIdx.x; i < A.material_count; i += RTW_BLOCK) mt[i] = w.materials[i];
-            if (A.sh_tex0 >= 0) {
-                int4* tx = reinterpret_cast<int4*>(smem + A.sh_tex0);
-                for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
-            }
-        }
-        __syncthreads();
-    } else if (LDS_SCENE) {
+    if (LDS_SCENE) {
         const float4* ga = sah ? w.sah_a : w.node_a;
         const float4* gb = sah ? w.sah_b : w.node_b;
         const float2* gk = sah ? w.sah_km : w.node_km;
@@ -1967,6 +1844,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     float pdot = 0.0f;  // dot((0,1,0), primary ray direction): the background's argument
     V3 att = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
     V3 psum = v3(0.0f, 0.0f, 0.0f);  // whole-pixel items: the pixel's running sum
+    uint32_t pcost = 0;               // ... and its deep paths' bounces (one atomic per pixel, not per path)
     int32_t depth = 0;
     Trav T;
     T.phase = PH_PIXEL;
@@ -2152,6 +2030,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         sample = big ? A.s_begin + ck * A.chunk : A.s_split + ck;
                         sample_end = big ? min(sample + A.chunk, A.s_split) : sample + 1;
                         psum = v3(0.0f, 0.0f, 0.0f);
+                        pcost = 0;
                         start_sample(1);
                         T.phase = PH_TRACE;
                     }
@@ -2182,7 +2061,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             T.node = w.root;
             if (sah) {  // the SAH walk needs the exact fast division; other rays take the reference tree
                 if (rp.fast) {
-                    T.node = LK == LK_SPHERES && A.sah4 ? w.sah4_root : w.sah_root;
+                    T.node = LK == LK_SPHERES && RTW_C2_PACKED && RTW_C2_INLINE ? w.sah_root_c2 : w.sah_root;
                     T.fast |= RTW_TF_SAH;
                 } else {
                     T.phase = PH_REF;
@@ -2205,13 +2084,9 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 #ifdef RTW_WAVE_TIMING
             uint64_t wx_t0 = wall_clock64();
 #endif
-            if (LDS_SCENE && LK == LK_SPHERES && A.sah4)
-                T = traverse4<STATS>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count, stack_off,
-                                     STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
-            else
-                T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
-                                                           A.leaf_count, A.rect_count, A.tri_count, stack_off,
-                                                           STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
+            T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
+                                                       A.leaf_count, A.rect_count, A.tri_count, stack_off,
+                                                       STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
             // the rays coop_trace takes (one call site, inlined: as an out-of-line call taking and
             // returning Trav by value it cost 304 B of scratch per lane, saved and restored around
             // every call -- suzanne's and cornell_cube's extra write traffic): the drain's last rays
@@ -2348,7 +2223,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 // deep paths (rare: trapped inside meshes, up to ~100x the mean cost) mark their
                 // slot for the next frame's work order
                 const int32_t bounces = A.max_depth - depth;
-                if (!STATS && A.slot_cost && bounces > 3) atomicAdd(&A.slot_cost[slot], (uint32_t)bounces);
+                if (!STATS && A.slot_cost && bounces > 3) {
+                    if (A.whole_pixel) pcost += (uint32_t)bounces;
+                    else atomicAdd(&A.slot_cost[slot], (uint32_t)bounces);
+                }
 #ifdef RTW_WAVE_TIMING
                 if (qfail >= RTW_QUEUES) {
                     ++wx_n;
@@ -2360,6 +2238,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 if (sample >= sample_end) {
                     T.phase = PH_PIXEL;
                     if (A.whole_pixel) {  // accumulate_kernel's last step, for this pixel
+                        if (!STATS && A.slot_cost && pcost) atomicAdd(&A.slot_cost[slot], pcost);
                         const V3 px = divs(psum, (float)A.spp);
                         float* o = A.layout == RTW_LAYOUT_TILES ? A.out + 3 * (size_t)slot : A.out + 3 * (size_t)pix;
                         o[0] = px.x;
@@ -2856,10 +2735,7 @@ struct SahTables {
     std::vector<float> km;        // cull constants, 2 per node
     std::vector<float4> box;      // 2 per leaf: the proof box (the leaf's parent box in the reference tree)
     std::vector<uint4> key;       // per leaf: its DFS key material (DWorld::leaf_key), empty if too deep
-    // the tree collapsed to 4 children per node (plain-sphere worlds; DWorld::sah4_*), empty if not made
-    std::vector<float4> a4, b4;
-    std::vector<int4> c4;
-    int32_t root4 = -1;
+    int32_t root_c2 = 0;  // the root's children, 16 + 16 bits (the two-children walk, plain-sphere worlds)
     int32_t root = 0, depth = 0;
     bool ok = false;
 };
@@ -2983,62 +2859,15 @@ SahTables build_sah_tables(const rtw_world* w) {
         S.a[i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
         S.b[i] = make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
     }
-    // 4-wide collapse for plain-sphere worlds (traverse4; RTW_SAH4=0 keeps the two-children walk): each
-    // node takes its two children and replaces the one with the largest box by its children until it has
-    // four (or only leaves); a leaf child's record is its sphere
-    bool spheres_only = true;
-    for (int32_t i = 0; i < L; ++i)
-        if (w->leaves[i].geom_kind != RTW_GEOM_SPHERE || w->leaves[i].flags != 0) spheres_only = false;
-    const char* e4 = std::getenv("RTW_SAH4");
-    if (spheres_only && (e4 && e4[0] == '1') && S.root >= 0) {
-        auto area = [&](int32_t n) {
-            const rtw_bvh_node& b = nodes[(size_t)n];
-            const double dx = (double)b.max[0] - b.min[0], dy = (double)b.max[1] - b.min[1], dz = (double)b.max[2] - b.min[2];
-            return dx * dy + dy * dz + dz * dx;
-        };
-        std::vector<std::pair<int32_t, int32_t>> todo{{S.root, 0}};  // (binary node, its 4-wide index)
-        S.c4.push_back(make_int4(0, 0, 0, 0));
-        S.a4.resize(4);
-        S.b4.resize(4);
-        S.root4 = 0;
-        while (!todo.empty()) {
-            const auto [n, q] = todo.back();
-            todo.pop_back();
-            std::vector<int32_t> ch{nodes[(size_t)n].left, nodes[(size_t)n].right};
-            while (ch.size() < 4) {
-                int best = -1;
-                double ba = -1.0;
-                for (size_t c = 0; c < ch.size(); ++c)
-                    if (ch[c] >= 0 && area(ch[c]) > ba) ba = area(ch[c]), best = (int)c;
-                if (best < 0) break;
-                const int32_t x = ch[(size_t)best];
-                ch.erase(ch.begin() + best);
-                ch.push_back(nodes[(size_t)x].left);
-                ch.push_back(nodes[(size_t)x].right);
-            }
-            int32_t cv[4] = {RTW_Q4_EMPTY, RTW_Q4_EMPTY, RTW_Q4_EMPTY, RTW_Q4_EMPTY};
-            for (size_t j = 0; j < ch.size(); ++j) {
-                const int32_t c = ch[j];
-                float4 ra = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rb = ra;
-                if (c < 0) {
-                    const rtw_sphere& sp = w->spheres[w->leaves[-1 - c].geom_index];
-                    ra = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius);
-                    cv[j] = c;
-                } else {
-                    const rtw_bvh_node& b = nodes[(size_t)c];
-                    ra = make_float4(b.min[0], b.min[1], b.min[2], b.max[0]);
-                    rb = make_float4(b.max[1], b.max[2], S.km[2 * (size_t)c], S.km[2 * (size_t)c + 1]);
-                    cv[j] = (int32_t)S.c4.size();
-                    todo.emplace_back(c, cv[j]);
-                    S.c4.push_back(make_int4(0, 0, 0, 0));
-                    S.a4.resize(S.a4.size() + 4);
-                    S.b4.resize(S.b4.size() + 4);
-                }
-                S.a4[4 * (size_t)q + j] = ra;
-                S.b4[4 * (size_t)q + j] = rb;
-            }
-            S.c4[(size_t)q] = make_int4(cv[0], cv[1], cv[2], cv[3]);
-        }
+    // plain-sphere worlds walk two children per step with the children packed 16 + 16 bits in the lane
+    // state and on the stack (traverse, C2P): their node and leaf indices must fit 16 bits
+    {
+        bool plain_spheres = true;
+        for (int32_t i = 0; i < L; ++i)
+            if (w->leaves[i].geom_kind != RTW_GEOM_SPHERE || w->leaves[i].flags != 0) plain_spheres = false;
+        if (plain_spheres && (nodes.size() >= 32767 || L >= 32767)) return S;
+        const rtw_bvh_node& r = nodes[(size_t)S.root];
+        S.root_c2 = (int32_t)(((uint32_t)r.left & 0xFFFFu) | ((uint32_t)r.right << 16));
     }
     S.box.resize((size_t)L * 2);
     for (int32_t i = 0; i < L; ++i) {
@@ -3099,7 +2928,6 @@ struct rtw_gpu_world {
     int32_t tri_count = 0, rect_count = 0, material_count = 0, texture_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int32_t sah_nodes = 0;  // nodes of the SAH tree, 0: the world takes the reference tree only (§5.6)
-    int32_t sah4_nodes = 0; // nodes of its 4-wide collapse (plain-sphere worlds), 0: none
     int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
     int32_t tex_kinds = TX_ANY;   // TX_*: the texture code the world's textures need
     int cus = 0;
@@ -3314,10 +3142,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     const size_t o_sk = sah.ok ? L.push(sah.km.data(), sah.km.size() * sizeof(float)) : 0;
     const size_t o_lb = sah.ok ? L.push(sah.box.data(), sah.box.size() * sizeof(float4)) : 0;
     const size_t o_lk = sah.ok && !sah.key.empty() ? L.push(sah.key.data(), sah.key.size() * sizeof(uint4)) : 0;
-    const bool q4 = sah.ok && !sah.c4.empty();
-    const size_t o_qa = q4 ? L.push(sah.a4.data(), sah.a4.size() * sizeof(float4)) : 0;
-    const size_t o_qb = q4 ? L.push(sah.b4.data(), sah.b4.size() * sizeof(float4)) : 0;
-    const size_t o_qc = q4 ? L.push(sah.c4.data(), sah.c4.size() * sizeof(int4)) : 0;
+
     WorldConst wcst;
     std::memset(&wcst, 0, sizeof(wcst));
     wcst.cam = w->camera;
@@ -3369,12 +3194,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         d.leaf_box = (const float4*)(base + o_lb);
         d.leaf_key = o_lk ? (const uint4*)(base + o_lk) : nullptr;
         d.sah_root = sah.root;
-        if (q4) {
-            d.sah4_a = (const float4*)(base + o_qa);
-            d.sah4_b = (const float4*)(base + o_qb);
-            d.sah4_c = (const int4*)(base + o_qc);
-            d.sah4_root = sah.root4;
-        }
+        d.sah_root_c2 = sah.root_c2;
     }
     d.has_light = w->has_light;
     d.wc = (const WorldConst*)(base + o_wc);
@@ -3390,7 +3210,6 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->depth = std::max(1, depth);
     if (sah.ok) {
         g->sah_nodes = (int32_t)sah.a.size();
-        g->sah4_nodes = (int32_t)sah.c4.size();
         g->depth = std::max(g->depth, sah.depth);
     }
     g->tri_count = w->triangle_count;
@@ -3665,21 +3484,14 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
     const size_t stack16_bytes = stack_bytes / 2;  // mode 2: 16-bit entries
     const char* lds_mode_env = std::getenv("RTW_LDS_MODE");  // audits: cap the mode
-    // the 4-wide walk (traverse4) where its tree exists (plain-sphere worlds) and fits in LDS (mode 1)
-    bool sah4 = sah && lk == LK_SPHERES && g->sah4_nodes > 0;
-    if (sah4 && ((size_t)(9 * g->sah4_nodes + g->leaf_count) * sizeof(float4) + stack_bytes > cap ||
-                 (lds_mode_env && std::atoi(lds_mode_env) < 1)))
-        sah4 = false;
-    A.sah4 = sah4 ? 1 : 0;
-    A.node_count = sah4 ? g->sah4_nodes : sah ? g->sah_nodes : g->node_count;
-    // LDS scene: 4-wide [a 4n][b 4n][children n][leaf records L], else [node_a n][node_b n][leaf records L]
-    // [cull constants (n + 1) / 2][rects 2R] (+ the triangle records in mode 2)
+    A.node_count = sah ? g->sah_nodes : g->node_count;
+    // LDS scene: [node_a n][node_b n][leaf records L][cull constants (n + 1) / 2][rects 2R] (+ the triangle
+    // records in mode 2)
     const size_t scene_bytes =
-        sah4 ? (size_t)(9 * A.node_count + g->leaf_count) * sizeof(float4)
-             : (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
-    A.fast_off = sah4 ? 9 * A.node_count : 2 * A.node_count;
+        (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
+    A.fast_off = 2 * A.node_count;
     int mode = 0;
-    if (!sah4 && g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 && A.node_count < 32768 &&
+    if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 && A.node_count < 32768 &&
         g->node_count < 32768 && scene_bytes + tri_bytes + stack16_bytes <= cap)
         mode = 2;
     else if (scene_bytes + stack_bytes <= cap) mode = 1;
@@ -3714,7 +3526,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         g->last_kernel[0] = mode;
         g->last_kernel[1] = lk;
         g->last_kernel[2] = tx;
-        g->last_kernel[3] = sah4 ? 2 : sah ? 1 : 0;  // 2: the 4-wide SAH walk
+        g->last_kernel[3] = sah ? 1 : 0;
     }
     const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

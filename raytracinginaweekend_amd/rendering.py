@@ -130,7 +130,7 @@ class DeviceWorld:
         m, lk, tx, tr = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         check(lib().rtw_world_kernel(self._h, C.byref(m), C.byref(lk), C.byref(tx), C.byref(tr)))
         return {"lds_mode": m.value, "leaf_kinds": lk.value, "tex_kinds": tx.value,
-                "tree": ("reference", "sah", "sah4")[tr.value] if tr.value >= 0 else None}
+                "tree": ("reference", "sah")[tr.value] if tr.value >= 0 else None}
 
     def collect_stats(self, params: N.RenderParams, tree: int = 0) -> dict:
         """Traversal statistics of one counting-variant render: tree 0 the reference's traversal

@@ -436,18 +436,16 @@ def test_whole_pixel_items_bit_exact(worlds, name, parts, monkeypatch):
         assert_bit_identical(img, ref, f"{name} whole-pixel items, {parts} partitions")
 
 
-@pytest.mark.parametrize("name", ["final_scene1", "defocus_blur", "perlin_spheres", "spheres_ties"])
-def test_sah4_walk_agrees(worlds, name, monkeypatch):
-    """the 4-wide SAH walk of plain-sphere worlds gives the two-children walk's bits
-    (RTW_SAH4=0) on a GPU-filling frame -- ties and grazing hits included (coincident and touching
-    spheres) -- and the oracle's on a small one."""
-    world = _tie_world(mesh=False) if name == "spheres_ties" else worlds(name)
-    monkeypatch.setenv("RTW_SAH4", "1")
-    assert _kernel_tree(world) == "sah4"
-    size = R.Size2i(320, 180)
-    four = R.render(size, 1, 8, 50, world, seed=47)
-    small = R.render(R.Size2i(48, 27), 1, 6, 50, world, seed=47)
-    assert_bit_identical(small, O.render(world, R.render_params(R.Size2i(48, 27), 6, 50, seed=47)), name)
-    monkeypatch.setenv("RTW_SAH4", "0")
+def test_two_children_walk_ties_and_grazing_hits(monkeypatch):
+    """The plain-sphere worlds' two-children SAH walk (its lane state and stack hold a node's children
+    packed 16 + 16 bits) on coincident spheres of different materials and touching spheres:
+    the oracle's bits, and the reference-tree loop's on a GPU-filling frame."""
+    world = _tie_world(mesh=False)
     assert _kernel_tree(world) == "sah"
-    assert_bit_identical(four, R.render(size, 1, 8, 50, world, seed=47), name + " 4-wide vs two-children walk")
+    size = R.Size2i(96, 54)
+    gpu = R.render(size, 1, 8, 50, world, seed=47)
+    assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=47)), "sphere tie world")
+    big = R.Size2i(480, 270)
+    sah = R.render(big, 1, 4, 50, world, seed=47)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert_bit_identical(sah, R.render(big, 1, 4, 50, world, seed=47), "sphere tie world, SAH vs reference tree")
