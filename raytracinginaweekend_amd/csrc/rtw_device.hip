@@ -82,7 +82,7 @@
 #define RTW_SAH_SPLIT_BUDGET 0.2  // spatial splits in the SAH tree of triangle worlds: extra references per leaf
 #endif
 #ifndef RTW_LDS_SCENE_MAX
-#define RTW_COOP_MAX 4       // drain: live lanes at most for the wave-cooperative trace (RTW_COOP_MAX=0: off)
+#define RTW_COOP_MAX 32      // drain: live lanes at most for the wave-cooperative trace (RTW_COOP_MAX=0: off); 4: suzanne -1.1 %, its 8-way shares up to 64.5 ms against 59.4 (profiles/r04/v3_experiments_ab.txt, v4_...)
 #define RTW_COOP_LEAVES 4096 // ... in worlds of at most this many leaves
 #define RTW_LDS_SCENE_MAX (160 * 1024)  // LDS bytes per block the scene (+ stack) may take
 #endif
@@ -440,6 +440,24 @@ __device__ __forceinline__ bool sphere_t(float4 s, const Ray& r, float ts, float
     return false;
 }
 
+// The same without branches (the two-children walk's RTW_C2_BRANCHLESS step): every operation runs, the
+// result is selected; the IEEE sqrt only in the rare 0 <= disc < 2^-96 (sqrt_nr's range ends there)
+__device__ __forceinline__ bool sphere_t_bf(float4 s, const Ray& r, float ts, float te, float& t) {
+    const V3 oc = sub(r.o, v3(s.x, s.y, s.z));
+    const float half_b = dot(oc, r.d);
+    const float c = dot(oc, oc) - s.w * s.w;
+    const float disc = half_b * half_b - c;
+    float sq = sqrt_nr(__builtin_fmaxf(disc, RTW_SQRT_LO));
+    if (__builtin_expect(disc >= 0.0f && disc < RTW_SQRT_LO, 0)) sq = __builtin_sqrtf(disc);
+    const float small = -half_b - sq;
+    const float large = -half_b + sq;
+    const bool ok = !(disc < 0.0f);
+    const bool hs = ok && contains(ts, te, small);
+    const bool hl = ok && contains(ts, te, large);
+    t = hs ? small : large;
+    return hs || hl;
+}
+
 __device__ __forceinline__ void rect_axes(int plane, int& p0, int& p1, int& n) {
     p0 = (plane == RTW_PLANE_YZ) ? 1 : 0;
     p1 = (plane == RTW_PLANE_XY) ? 1 : 2;
@@ -567,6 +585,12 @@ __device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i
 // conflict cycles per LDS instruction in round 2).  Worlds of at most RTW_TRI_SOA triangles.
 #ifndef RTW_TRI_SOA
 #define RTW_TRI_SOA 1024
+#endif
+// ... and indexed by leaf, not by triangle (RTW_TRI_BY_LEAF): a leaf step then loads the record at the
+// leaf's own index, at once with the leaf record that says it is a triangle, instead of after it (one
+// dependent LDS read less per triangle test; worlds of at most RTW_TRI_SOA leaves)
+#ifndef RTW_TRI_BY_LEAF
+#define RTW_TRI_BY_LEAF 1
 #endif
 __device__ __forceinline__ TriFast load_tri_soa(const float4* __restrict__ tf, int i) {
     const float4 a = tf[i], b = tf[RTW_TRI_SOA + i], c = tf[2 * RTW_TRI_SOA + i], d = tf[3 * RTW_TRI_SOA + i];
@@ -1497,6 +1521,11 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // one leaf's test at the current t range (hittable.rs:436-437: a leaf is never box-tested)
     auto test_leaf = [&](int leaf) {
         const float4 sph = fast[leaf];
+        // mode 2 with leaf-indexed triangle records: load the record with the leaf record, before the
+        // leaf's kind is known (a sphere or rect leaf reads an unused slot)
+        constexpr bool TRI_EARLY = RTW_TRI_BY_LEAF && LDS == 2 && LDS_SCENE && (LK == LK_TRIS || LK == LK_PLAIN);
+        TriFast tfe;
+        if (TRI_EARLY) tfe = load_tri_soa(tri_fast, leaf);
         if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
             if (STATS) st.c[ST_T_SPHERE]++;
             float t;
@@ -1514,7 +1543,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             if (STATS) st.c[ST_T_TRI]++;
             float t;
             const int ti = __float_as_int(sph.y);
-            if (tri_test(LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), T.ray, 0.001f, T.te, t))
+            if (tri_test(TRI_EARLY ? tfe : LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, RTW_TRI_BY_LEAF ? leaf : ti)
+                                                 : load_tri(tri_fast, ti),
+                         T.ray, 0.001f, T.te, t))
                 take(t, leaf);
         } else if (LK >= LK_WRAPPED) {
             float t;
@@ -1608,7 +1639,26 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             float el, er;
             bool pl, pr;
             int32_t lc = left, rc = right;  // what stands for an accepted child: C2P its children, else itself
-            if (C2_INLINE) {
+#ifndef RTW_C2_BRANCHLESS
+#define RTW_C2_BRANCHLESS 0
+#endif
+            if (C2_INLINE && RTW_C2_BRANCHLESS && !STATS) {
+                // both tests for both children, selected: no exec-mask branches (lanes mix leaf and
+                // internal children at almost every step, so the branchy form runs both anyway)
+                const int32_t ll = left < 0 ? -1 - left : 0, rl = right < 0 ? -1 - right : 0;
+                float t0, t1;
+                const bool h0 = sphere_t_bf(fast[ll], T.ray, 0.001f, T.te, t0) && left < 0;
+                if (h0) take(t0, ll);
+                const bool h1 = sphere_t_bf(fast[rl], T.ray, 0.001f, T.te, t1) && right < 0;
+                if (h1) take(t1, rl);
+                const float4 lb = nodes_b[il], rb = nodes_b[ir];
+                pl = node_pass_cons<SAH_DQ>(nodes_a[il], lb, nkm[il], T.ray, rp, 0.001f, T.te, el) && left >= 0;
+                pr = node_pass_cons<SAH_DQ>(nodes_a[ir], rb, nkm[ir], T.ray, rp, 0.001f, T.te, er) && right >= 0;
+                if (C2P) {
+                    lc = pack2(lb);
+                    rc = pack2(rb);
+                }
+            } else if (C2_INLINE) {
                 // leaf children: their sphere now (never pushed or visited); internal ones: the box
                 pl = pr = false;
                 el = er = F32_INF;
@@ -1744,7 +1794,8 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
                 hit = rect_t_mk(g, r, inv, 0.001f, F32_INF, t);  // SAH rays are Markstein-exact
             } else {
                 const int ti = __float_as_int(sph.y);
-                hit = tri_test(LDS == 2 ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), r, 0.001f, F32_INF, t);
+                hit = tri_test(LDS == 2 ? load_tri_soa(tri_fast, RTW_TRI_BY_LEAF ? leaf : ti) : load_tri(tri_fast, ti), r, 0.001f,
+                               F32_INF, t);
             }
             if (hit) {
                 cnt = t == best ? cnt + 1 : t < best ? 1u : cnt;
@@ -1812,7 +1863,17 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         for (int i = threadIdx.x; i < 2 * A.rect_count; i += RTW_BLOCK) rects[i] = w.rects[i];
         if (LDS == 2) {
             float4* tris = rects + 2 * A.rect_count;
-            for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[(i & 3) * RTW_TRI_SOA + (i >> 2)] = w.tri_fast[i];
+            if (RTW_TRI_BY_LEAF) {  // component k of plain-triangle leaf l at k * RTW_TRI_SOA + l
+                for (int l = threadIdx.x; l < A.leaf_count; l += RTW_BLOCK) {
+                    const float4 f = w.leaf_fast[l];
+                    if (f.w != f.w && __float_as_int(f.x) == 1) {
+                        const int ti = __float_as_int(f.y);
+                        for (int k = 0; k < 4; ++k) tris[k * RTW_TRI_SOA + l] = w.tri_fast[4 * ti + k];
+                    }
+                }
+            } else {
+                for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[(i & 3) * RTW_TRI_SOA + (i >> 2)] = w.tri_fast[i];
+            }
         }
         if (A.sh_li >= 0) {  // shading tables (launch_render decides whether they fit)
             int4* li = reinterpret_cast<int4*>(smem + A.sh_li);
@@ -2818,7 +2879,7 @@ SahTables build_sah_tables(const rtw_world* w) {
                 if (!coord_ok(nd.min[k2]) || !coord_ok(nd.max[k2])) ok = false;
         // the extra nodes must not push a mesh world out of LDS mode 2 (its triangle records in LDS;
         // launch_render's sizing with the plain tree's depth as a floor): else the plain tree
-        if (ok && w->triangle_count <= RTW_TRI_SOA) {
+        if (ok && (RTW_TRI_BY_LEAF ? L : w->triangle_count) <= RTW_TRI_SOA) {
             int32_t proot = 0;
             int pdepth = 0;
             std::vector<rtw_bvh_node> plain;
@@ -3491,7 +3552,8 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
     A.fast_off = 2 * A.node_count;
     int mode = 0;
-    if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 && A.node_count < 32768 &&
+    if (g->tri_count > 0 && (RTW_TRI_BY_LEAF ? g->leaf_count : g->tri_count) <= RTW_TRI_SOA && g->leaf_count < 32768 &&
+        A.node_count < 32768 &&
         g->node_count < 32768 && scene_bytes + tri_bytes + stack16_bytes <= cap)
         mode = 2;
     else if (scene_bytes + stack_bytes <= cap) mode = 1;
