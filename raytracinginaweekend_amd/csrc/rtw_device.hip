@@ -440,24 +440,6 @@ __device__ __forceinline__ bool sphere_t(float4 s, const Ray& r, float ts, float
     return false;
 }
 
-// The same without branches (the two-children walk's RTW_C2_BRANCHLESS step): every operation runs, the
-// result is selected; the IEEE sqrt only in the rare 0 <= disc < 2^-96 (sqrt_nr's range ends there)
-__device__ __forceinline__ bool sphere_t_bf(float4 s, const Ray& r, float ts, float te, float& t) {
-    const V3 oc = sub(r.o, v3(s.x, s.y, s.z));
-    const float half_b = dot(oc, r.d);
-    const float c = dot(oc, oc) - s.w * s.w;
-    const float disc = half_b * half_b - c;
-    float sq = sqrt_nr(__builtin_fmaxf(disc, RTW_SQRT_LO));
-    if (__builtin_expect(disc >= 0.0f && disc < RTW_SQRT_LO, 0)) sq = __builtin_sqrtf(disc);
-    const float small = -half_b - sq;
-    const float large = -half_b + sq;
-    const bool ok = !(disc < 0.0f);
-    const bool hs = ok && contains(ts, te, small);
-    const bool hl = ok && contains(ts, te, large);
-    t = hs ? small : large;
-    return hs || hl;
-}
-
 __device__ __forceinline__ void rect_axes(int plane, int& p0, int& p1, int& n) {
     p0 = (plane == RTW_PLANE_YZ) ? 1 : 0;
     p1 = (plane == RTW_PLANE_XY) ? 1 : 2;
@@ -586,11 +568,11 @@ __device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i
 #ifndef RTW_TRI_SOA
 #define RTW_TRI_SOA 1024
 #endif
-// ... and indexed by leaf, not by triangle (RTW_TRI_BY_LEAF): a leaf step then loads the record at the
-// leaf's own index, at once with the leaf record that says it is a triangle, instead of after it (one
-// dependent LDS read less per triangle test; worlds of at most RTW_TRI_SOA leaves)
+// RTW_TRI_BY_LEAF=1 builds index them by leaf instead and load a leaf's record with its leaf record,
+// before knowing it is a triangle: one dependent LDS read less per triangle test, but suzanne -1.8 %
+// (the early record's 16 VGPRs; profiles/r04/v5_experiments_ab.txt)
 #ifndef RTW_TRI_BY_LEAF
-#define RTW_TRI_BY_LEAF 1
+#define RTW_TRI_BY_LEAF 0
 #endif
 __device__ __forceinline__ TriFast load_tri_soa(const float4* __restrict__ tf, int i) {
     const float4 a = tf[i], b = tf[RTW_TRI_SOA + i], c = tf[2 * RTW_TRI_SOA + i], d = tf[3 * RTW_TRI_SOA + i];
@@ -982,7 +964,18 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
 // (sah_delta), so w_i here >= (17/16)(1 - 4u) w_i of the exact test: each bound of this interval
 // lies outside the exact test's bound (RN is monotone), and this test passes every node that
 // test passes.  One multiply per quotient instead of three operations.
+// RTW_SAH_SPACE_MARGIN builds grow the box in space instead (a_i - delta, b_i + delta, then the cheap
+// quotients): three operations less per box, but the subtraction's rounding (u |a_i| more) needs the
+// constants widened by 9/8: the errors total 5u |a_i| + 6u delta <= 0.079 delta against the margin
+// delta / 8 (delta >= 64u D >= 64u |a_i|)
+#ifndef RTW_SAH_SPACE_MARGIN
+#define RTW_SAH_SPACE_MARGIN 0
+#endif
+#if RTW_SAH_SPACE_MARGIN
+#define RTW_SAH_WIDEN (9.0f / 8.0f)
+#else
 #define RTW_SAH_WIDEN (17.0f / 16.0f)
+#endif
 // DQ = false (the product): the k term takes D^2 >= Dq, so delta = fma(D, fma(k, D, 68u), m): two
 // operations for five, and a delta at least as large up to two roundings (the containment argument's
 // margin is 17/16 against 1 + 3/64; tests/test_gpu_node_pass.py checks both forms)
@@ -1003,6 +996,19 @@ __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, 
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
     const float delta = sah_delta<DQ>(km.x, km.y, a0, b0, a1, b1, a2, b2);
+#if RTW_SAH_SPACE_MARGIN && !defined(RTW_SAH_EXACT_Q)
+    if (!DQ) {
+        const float qa0 = (a0 - delta) * rp.inv.x, qb0 = (b0 + delta) * rp.inv.x;
+        const float qa1 = (a1 - delta) * rp.inv.y, qb1 = (b1 + delta) * rp.inv.y;
+        const float qa2 = (a2 - delta) * rp.inv.z, qb2 = (b2 + delta) * rp.inv.z;
+        const float lo = __builtin_fmaxf(
+            __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(qa0, qb0), __builtin_fminf(qa1, qb1)), __builtin_fminf(qa2, qb2)), ts);
+        const float hi = __builtin_fminf(
+            __builtin_fminf(__builtin_fminf(__builtin_fmaxf(qa0, qb0), __builtin_fmaxf(qa1, qb1)), __builtin_fmaxf(qa2, qb2)), te);
+        entry = lo;
+        return !(lo > hi);
+    }
+#endif
 #ifdef RTW_SAH_EXACT_Q  // audit / A/B builds: the exact quotients of the reference tree's test
     const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
     const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
@@ -1510,6 +1516,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 #else
     constexpr bool SAH_DQ = false;
 #endif
+    // (reading the stack's top as each step starts, so that a pop finds it arrived, lost 0.4-2.3 %:
+    // profiles/r04/v6_spec_pop_ab.txt)
     auto pop = [&]() {
         if (T.sp == 0) T.phase = PH_SHADE;
         else T.node = stack[(--T.sp) * RTW_BLOCK];
@@ -1639,26 +1647,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             float el, er;
             bool pl, pr;
             int32_t lc = left, rc = right;  // what stands for an accepted child: C2P its children, else itself
-#ifndef RTW_C2_BRANCHLESS
-#define RTW_C2_BRANCHLESS 0
-#endif
-            if (C2_INLINE && RTW_C2_BRANCHLESS && !STATS) {
-                // both tests for both children, selected: no exec-mask branches (lanes mix leaf and
-                // internal children at almost every step, so the branchy form runs both anyway)
-                const int32_t ll = left < 0 ? -1 - left : 0, rl = right < 0 ? -1 - right : 0;
-                float t0, t1;
-                const bool h0 = sphere_t_bf(fast[ll], T.ray, 0.001f, T.te, t0) && left < 0;
-                if (h0) take(t0, ll);
-                const bool h1 = sphere_t_bf(fast[rl], T.ray, 0.001f, T.te, t1) && right < 0;
-                if (h1) take(t1, rl);
-                const float4 lb = nodes_b[il], rb = nodes_b[ir];
-                pl = node_pass_cons<SAH_DQ>(nodes_a[il], lb, nkm[il], T.ray, rp, 0.001f, T.te, el) && left >= 0;
-                pr = node_pass_cons<SAH_DQ>(nodes_a[ir], rb, nkm[ir], T.ray, rp, 0.001f, T.te, er) && right >= 0;
-                if (C2P) {
-                    lc = pack2(lb);
-                    rc = pack2(rb);
-                }
-            } else if (C2_INLINE) {
+            if (C2_INLINE) {
                 // leaf children: their sphere now (never pushed or visited); internal ones: the box
                 pl = pr = false;
                 el = er = F32_INF;
@@ -1726,7 +1715,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             } else if (T.sp == 0) {
                 T.phase = PH_SHADE;
             } else {
-                T.node = stack[(--T.sp) * RTW_BLOCK];
+                pop();
             }
         }
         }
