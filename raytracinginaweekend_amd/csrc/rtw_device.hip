@@ -369,6 +369,96 @@ __device__ __forceinline__ V3 refract(V3 d, V3 n, float eta) {  // vec3.rs:235-2
 #define F32_TAU 6.28318548202514648438f
 #define F32_INF (__builtin_inff())
 
+// The RNG draws of the path (rtw_scalar.h: rand_xoshiro 0.6's Xoroshiro128PlusPlus, rand 0.8.5's
+// UniformFloat, rand_distr 0.4.3's UnitDisc / UnitSphere / UnitBall), written for gfx950: the same
+// values with fewer instructions.  A wave runs a rejection loop as many rounds as its unluckiest lane
+// needs, so each draw's cost is paid several times over.
+// * a 64-bit rotation by a constant is two v_alignbit_b32 (the compiler's 64-bit shifts and an or: 3);
+// * rand's [0, 1) float (u >> 9 | bits(1.0f)) - 1 takes its or from the alignbit's high word:
+//   alignbit(0x7F, u, 9) = u >> 9 | 0x7F << 23; and UnitDisc / UnitSphere / UnitBall's
+//   Uniform(-1, 1) sample v * 2 + (-1) is bits(u >> 9 | 0x40000000) - 3 = 2 (1 + m) - 3, one
+//   subtraction: both are 2 m - 1 exactly (m = (u >> 9) 2^-23; 2 m - 1 is a multiple of 2^-23 in
+//   [-1, 1), so neither form rounds);
+// * UnitSphere's sqrt(1 - sum) is sqrt_nr: 2^-24 <= 1 - sum <= 1 (sum is a float below 1).
+// Every image test draws through these (parity suite: all samplers, all worlds).
+__device__ __forceinline__ uint64_t d_rotl64(uint64_t x, int k) {  // k: a constant in 1..63, not 32
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    uint32_t nlo, nhi;
+    if (k < 32) {
+        nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - k);
+        nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - k);
+    } else {
+        nhi = __builtin_amdgcn_alignbit(lo, hi, 64 - k);
+        nlo = __builtin_amdgcn_alignbit(hi, lo, 64 - k);
+    }
+    return ((uint64_t)nhi << 32) | nlo;
+}
+// (RTW_DEV_RNG=0 builds draw through rtw_scalar.h's functions instead: the A/B baseline)
+#ifndef RTW_DEV_RNG
+#define RTW_DEV_RNG 1
+#endif
+__device__ __forceinline__ uint64_t d_next_u64(rtw_xoro* r) {  // rtw_xoro_next_u64
+    if (!RTW_DEV_RNG) return rtw_xoro_next_u64(r);
+    const uint64_t s0 = r->s0;
+    uint64_t s1 = r->s1;
+    const uint64_t result = d_rotl64(s0 + s1, 17) + s0;
+    s1 ^= s0;
+    r->s0 = d_rotl64(s0, 49) ^ s1 ^ (s1 << 21);
+    r->s1 = d_rotl64(s1, 28);
+    return result;
+}
+__device__ __forceinline__ uint32_t d_next_u32(rtw_xoro* r) { return (uint32_t)d_next_u64(r); }
+__device__ __forceinline__ float d_value0_1(uint32_t u) {
+    if (!RTW_DEV_RNG) return rtw_value0_1(u);
+    return __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, u, 9)) - 1.0f;
+}
+__device__ __forceinline__ float d_m1_1(rtw_xoro* r) {  // rtw_uniform_m1_1
+    if (!RTW_DEV_RNG) return rtw_uniform_m1_1(r);
+    return __uint_as_float(__builtin_amdgcn_alignbit(0x80u, d_next_u32(r), 9)) - 3.0f;
+}
+__device__ __forceinline__ float d_gen_f32(rtw_xoro* r) {  // rtw_gen_f32
+    return (1.0f / 16777216.0f) * (float)(d_next_u32(r) >> 8);
+}
+__device__ __forceinline__ bool d_gen_bool_half(rtw_xoro* r) { return d_next_u64(r) < 0x8000000000000000ull; }
+__device__ __forceinline__ float d_uniform_sample(const rtw_uniform& u, rtw_xoro* r) {  // rtw_uniform_sample
+    return d_value0_1(d_next_u32(r)) * u.scale + u.low;
+}
+__device__ __forceinline__ float d_gen_range_f32(float low, float high, rtw_xoro* r) {  // rtw_gen_range_f32
+    const float scale = high - low;
+    for (;;) {
+        const float res = d_value0_1(d_next_u32(r)) * scale + low;
+        if (res < high) return res;
+    }
+}
+__device__ __forceinline__ void d_unit_disc(rtw_xoro* r, float& x1, float& x2) {  // rtw_unit_disc
+    for (;;) {
+        x1 = d_m1_1(r);
+        x2 = d_m1_1(r);
+        if (x1 * x1 + x2 * x2 <= 1.0f) break;
+    }
+}
+__device__ __forceinline__ V3 d_unit_sphere(rtw_xoro* r) {  // rtw_unit_sphere
+    float x1, x2, sum;
+    for (;;) {
+        x1 = d_m1_1(r);
+        x2 = d_m1_1(r);
+        sum = x1 * x1 + x2 * x2;
+        if (sum < 1.0f) break;
+    }
+    const float factor = 2.0f * (RTW_DEV_RNG ? sqrt_nr(1.0f - sum) : __builtin_sqrtf(1.0f - sum));
+    return v3(x1 * factor, x2 * factor, 1.0f - 2.0f * sum);
+}
+__device__ __forceinline__ V3 d_unit_ball(rtw_xoro* r) {  // rtw_unit_ball
+    float x1, x2, x3;
+    for (;;) {
+        x1 = d_m1_1(r);
+        x2 = d_m1_1(r);
+        x3 = d_m1_1(r);
+        if (x1 * x1 + x2 * x2 + x3 * x3 <= 1.0f) break;
+    }
+    return v3(x1, x2, x3);
+}
+
 // Out-of-line wrappers: the f64 polynomial constants need SGPR pairs (no VOP3 literals on
 // gfx9); inlined into the bounce loop they get hoisted and pin ~100 SGPRs.
 __device__ __noinline__ float d_acosf(float x) { return rtw_acosf(x); }
@@ -723,7 +813,7 @@ __device__ __forceinline__ bool leaf_t(const DWorld& w, int leaf, const Ray& r, 
         const float em = rtw_minr(tt, te);
         if (sm >= em) return false;
         const float nid = w.leaf_xf[3 * leaf].x;
-        const float tv = rtw_maxr(sm, 0.0f) + nid * d_logf(rtw_gen_f32(&rng));
+        const float tv = rtw_maxr(sm, 0.0f) + nid * d_logf(d_gen_f32(&rng));
         if (tv > em) return false;
         t = tv;
         return true;
@@ -964,18 +1054,10 @@ __device__ __forceinline__ bool node_pass(float4 na, float4 nb, float2 km, const
 // (sah_delta), so w_i here >= (17/16)(1 - 4u) w_i of the exact test: each bound of this interval
 // lies outside the exact test's bound (RN is monotone), and this test passes every node that
 // test passes.  One multiply per quotient instead of three operations.
-// RTW_SAH_SPACE_MARGIN builds grow the box in space instead (a_i - delta, b_i + delta, then the cheap
-// quotients): three operations less per box, but the subtraction's rounding (u |a_i| more) needs the
-// constants widened by 9/8: the errors total 5u |a_i| + 6u delta <= 0.079 delta against the margin
-// delta / 8 (delta >= 64u D >= 64u |a_i|)
-#ifndef RTW_SAH_SPACE_MARGIN
-#define RTW_SAH_SPACE_MARGIN 0
-#endif
-#if RTW_SAH_SPACE_MARGIN
-#define RTW_SAH_WIDEN (9.0f / 8.0f)
-#else
+// (Growing the box in space instead -- a_i - delta, b_i + delta, then the quotients: three operations less
+// per box, the constants widened by 9/8 for the subtraction's rounding -- passed the containment and
+// parity suites and was not faster: suzanne -0.5 %, profiles/r04/v7_space_margin_ab.txt.)
 #define RTW_SAH_WIDEN (17.0f / 16.0f)
-#endif
 // DQ = false (the product): the k term takes D^2 >= Dq, so delta = fma(D, fma(k, D, 68u), m): two
 // operations for five, and a delta at least as large up to two roundings (the containment argument's
 // margin is 17/16 against 1 + 3/64; tests/test_gpu_node_pass.py checks both forms)
@@ -996,19 +1078,6 @@ __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, 
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
     const float delta = sah_delta<DQ>(km.x, km.y, a0, b0, a1, b1, a2, b2);
-#if RTW_SAH_SPACE_MARGIN && !defined(RTW_SAH_EXACT_Q)
-    if (!DQ) {
-        const float qa0 = (a0 - delta) * rp.inv.x, qb0 = (b0 + delta) * rp.inv.x;
-        const float qa1 = (a1 - delta) * rp.inv.y, qb1 = (b1 + delta) * rp.inv.y;
-        const float qa2 = (a2 - delta) * rp.inv.z, qb2 = (b2 + delta) * rp.inv.z;
-        const float lo = __builtin_fmaxf(
-            __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(qa0, qb0), __builtin_fminf(qa1, qb1)), __builtin_fminf(qa2, qb2)), ts);
-        const float hi = __builtin_fminf(
-            __builtin_fminf(__builtin_fminf(__builtin_fmaxf(qa0, qb0), __builtin_fmaxf(qa1, qb1)), __builtin_fmaxf(qa2, qb2)), te);
-        entry = lo;
-        return !(lo > hi);
-    }
-#endif
 #ifdef RTW_SAH_EXACT_Q  // audit / A/B builds: the exact quotients of the reference tree's test
     const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
     const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
@@ -1154,8 +1223,8 @@ __device__ __forceinline__ V3 light_generate(const rtw_rect& g, V3 origin, rtw_x
     int p0, p1, n;
     rect_axes(g.plane, p0, p1, n);
     V3 e = v3(0.0f, 0.0f, 0.0f);
-    setc(e, p0, rtw_gen_range_f32(g.r0[0], g.r0[1], &rng));
-    setc(e, p1, rtw_gen_range_f32(g.r1[0], g.r1[1], &rng));
+    setc(e, p0, d_gen_range_f32(g.r0[0], g.r0[1], &rng));
+    setc(e, p1, d_gen_range_f32(g.r1[0], g.r1[1], &rng));
     setc(e, n, g.dist);
     return unit_x(sub(e, origin));
 }
@@ -1193,13 +1262,13 @@ __device__ __forceinline__ V3 background(const rtw_background& bg, float pdot) {
 __device__ __forceinline__ Ray camera_ray(const rtw_camera& c, rtw_xoro& rng, float px, float py) {
     V3 off = v3(0.0f, 0.0f, 0.0f);
     if (c.lens_radius > 0.0f) {
-        float d[2];
-        rtw_unit_disc(&rng, d);
-        off = mul(add(mul(ld3(c.unit_right), d[0]), mul(ld3(c.unit_up), d[1])), c.lens_radius);
+        float d0, d1;
+        d_unit_disc(&rng, d0, d1);
+        off = mul(add(mul(ld3(c.unit_right), d0), mul(ld3(c.unit_up), d1)), c.lens_radius);
     }
     float start;
     if (c.time0 == c.time1) start = c.time0;
-    else start = rtw_gen_range_f32(c.time0, c.time1, &rng);
+    else start = d_gen_range_f32(c.time0, c.time1, &rng);
     Ray r;
     r.time = start + (c.shutter_pace[0] * px + c.shutter_pace[1] * py);
     r.o = add(ld3(c.position), off);
@@ -1289,11 +1358,10 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                     const float fuzz = __int_as_float(M.z);
                     V3 fz = v3(0.0f, 0.0f, 0.0f);
                     if (fuzz > 0.0f) {
-                        float b[3];
                         RTW_PT(6);
-                        rtw_unit_ball(&rng, b);
+                        const V3 b = d_unit_ball(&rng);
                         RTW_PT(4);
-                        fz = mul(v3(b[0], b[1], b[2]), fuzz);
+                        fz = mul(b, fuzz);
                     }
                     const V3 dir = add(reflect(ray.d, h.n), fz);
                     if (dot(dir, h.n) > 0.0f) {
@@ -1314,7 +1382,7 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                         const float x = 1.0f - cos_t;
                         const float x2 = x * x;
                         const float p5 = x * (x2 * x2);  // powi(5)
-                        refl = (rs + (1.0f - rs) * p5) > rtw_gen_f32(&rng);
+                        refl = (rs + (1.0f - rs) * p5) > d_gen_f32(&rng);
                     }
                     sdir = unit_x(refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio));
                 } else if (mkind == RTW_MAT_ISOTROPIC) {
@@ -1329,14 +1397,12 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                 bool light_dir = false;
                 RTW_PT(6);
                 if (cosine) {
-                    if (w.has_light) light_dir = rtw_gen_bool_half(&rng);
+                    if (w.has_light) light_dir = d_gen_bool_half(&rng);
                     need_sphere = !light_dir;
                 }
                 if (light_dir) sdir = light_generate(w.wc->light, h.pos, rng);
                 if (need_sphere) {
-                    float s[3];
-                    rtw_unit_sphere(&rng, s);
-                    const V3 sv = v3(s[0], s[1], s[2]);
+                    const V3 sv = d_unit_sphere(&rng);
                     if (cosine) {  // (n + UnitSphere).unit_or_else(n) (material.rs:20-22)
                         const V3 v = add(h.n, sv);
                         const float lsq = dot(v, v);
@@ -1913,8 +1979,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         (void)back;
         RTW_PT(5);
         T.rng = rtw_sample_stream(A.seed_key, pix, sample);
-        const float jx = rtw_uniform_sample(&A.ux, &T.rng);
-        const float jy = rtw_uniform_sample(&A.uy, &T.rng);
+        const float jx = d_uniform_sample(A.ux, &T.rng);
+        const float jy = d_uniform_sample(A.uy, &T.rng);
         T.ray = camera_ray(w.wc->cam, T.rng, fx + jx, fy + jy);
         pdot = dot(v3(0.0f, 1.0f, 0.0f), T.ray.d);  // background_color.rs:13 on the primary ray
         att = v3(1.0f, 1.0f, 1.0f);
