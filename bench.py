@@ -184,7 +184,13 @@ def render_configs(args, local_rank: int, steps: int, warmup: int, barrier) -> l
             rec.update({"value": round(w * h * spp / dt / 1e6, 3), "unit": "Msamples/sec", "steps": steps,
                         "warmup": warmup, "ms_per_step": round(dt * 1e3, 3),
                         "kernel_ms": round(st.elapsed_time(en) / steps, 3)})
-        rec.update({"trace_min": fr.dworld.tuned_trace_min(), "kernel": fr.dworld.kernel_variant()})
+        lf = fr.dworld.last_frame()
+        rec.update({"trace_min": lf["trace_min"],
+                    "kernel": fr.dworld.kernel_variant(), "launches_per_frame": lf["launches"],
+                    "work_items": "whole pixels" if lf["whole_pixel"] else "samples",
+                    # the per-sample colour records the frame writes (whole-pixel items: none, the
+                    # pixels themselves, 12 B each)
+                    "colour_record_bytes": (w * h * 12) if lf["whole_pixel"] else (w * h * spp * 12)})
         out.append(rec)
         fr.dworld.release()
         del fr, world
@@ -547,8 +553,6 @@ def main() -> int:
     configs = None
     if rank == 0 and world_size == 1 and not args.no_configs:
         configs = render_configs(args, local_rank, max(1, args.configs_steps), 1, barrier)
-        for (name, w, h, spp, _), r in zip(CONFIG_LEGS, configs):
-            r["colour_record_bytes"] = w * h * spp * 12
         if not args.no_pmc:
             configs_pmc(args, configs, peak_ginstr)
 
@@ -585,8 +589,10 @@ def main() -> int:
                 "max_depth": args.max_depth,
                 "partition": f"interleaved {spec.tile[0]}x{spec.tile[1]} tiles over {world_size} GPU(s)",
                 "rccl_world_size": world_size,
-                "trace_min": fr.dworld.tuned_trace_min(),
+                "trace_min": fr.dworld.last_frame()["trace_min"],
                 "kernel": fr.dworld.kernel_variant(),
+                "launches_per_frame": fr.dworld.last_frame()["launches"],
+                "work_items": "whole pixels" if fr.dworld.last_frame()["whole_pixel"] else "samples",
             },
             "first_frame_ms": first_frame_ms,
             "first_frame_Msamples_s": round(args.width * args.height * args.spp / first_frame_ms / 1e3, 1)

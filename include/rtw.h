@@ -269,6 +269,12 @@ RTW_API int rtw_world_tuning(rtw_gpu_world* gw, int* trace_min);
  * the reference-order proof and fallback); -1 each before the first render.
  * Diagnostics only. */
 RTW_API int rtw_world_kernel(rtw_gpu_world* gw, int* lds_mode, int* leaf_kinds, int* tex_kinds, int* tree);
+/* The shape of this world's last frame (rtw_render_device / rtw_render on it): render-kernel launches,
+ * whether the work items were whole pixels (1: samples summed in registers, no colour buffer, DESIGN.md
+ * 5.5b; 0: single samples through the colour buffer), and the dynamic-fetch threshold it ran with (the
+ * world's tuned one once chosen, else the default: 32, 16 for whole-pixel frames, or RTW_TRACE_MIN);
+ * -1 each before the first frame.  Synchronous; diagnostics only. */
+RTW_API int rtw_world_last_frame(rtw_gpu_world* gw, int* launches, int* whole_pixel, int* trace_min);
 /* Renders this partition's tiles into device buffer `d_out` (layout per params->layout) on
  * `stream` (a hipStream_t, NULL = default stream).  Asynchronous: returns after the launch. */
 RTW_API int rtw_render_device(rtw_gpu_world* gw, const rtw_render_params* params, float* d_out,

@@ -215,6 +215,7 @@ struct KArgs {
     // shading tables in LDS (float4 offsets, -1: read from HBM / L2): leaf records, materials and, in
     // solid-texture worlds, each texture's first record; the stack follows them (stack_off)
     int32_t sh_li, sh_mat, sh_tex0, stack_off;
+    int32_t sh_box;  // the leaves' proof boxes (2 float4 each) in LDS after the shading tables, -1: HBM / L2
     int32_t material_count, texture_count;
     int32_t fast_off;         // LDS float4 offset of the leaf records (leaf_fast)
     int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
@@ -1812,6 +1813,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 // decides as for any hit; a lane holding two tied leaves keeps the flag (re-traced on the reference
 // tree).  Rays of `todo` only (SAH rays: RTW_TF_SAH).  `audit` (tests only, RTW_COOP_AUDIT=1) takes
 // the DFS-last tied leaf instead: wrong images, which shows that the resolution decides them.
+#ifndef RTW_COOP_PIPE
+#define RTW_COOP_PIPE 1
+#endif
 template <int LDS, int LK>
 __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, unsigned long long todo, int32_t n_nodes,
                                         int32_t n_leaves, int32_t n_rects, int32_t fast_off, bool audit) {
@@ -1836,8 +1840,19 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
         float best = F32_INF;
         int32_t bl = -1;
         uint32_t cnt = 0;  // leaves of this lane reporting exactly `best`
+        // software-pipelined: the next leaf record is read before this leaf's test, so that its LDS
+        // latency overlaps the triangle / rect record read that depends on this one (one round trip per
+        // leaf instead of two; the drain's rays are latency-bound, one at a time per wave)
+#if RTW_COOP_PIPE
+        float4 sph_n = lane < n_leaves ? fast[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#endif
         for (int32_t leaf = lane; leaf < n_leaves; leaf += 64) {
+#if RTW_COOP_PIPE
+            const float4 sph = sph_n;
+            if (leaf + 64 < n_leaves) sph_n = fast[leaf + 64];
+#else
             const float4 sph = fast[leaf];
+#endif
             float t;
             bool hit;
             if (LK == LK_SPHERES || sph.w == sph.w) {
@@ -1935,6 +1950,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) li[i] = w.leaf_info[i];
             int4* mt = reinterpret_cast<int4*>(smem + A.sh_mat);
             for (int i = threadIdx.x; i < A.material_count; i += RTW_BLOCK) mt[i] = w.materials[i];
+            if (A.sh_box >= 0)
+                for (int i = threadIdx.x; i < 2 * A.leaf_count; i += RTW_BLOCK) smem[A.sh_box + i] = w.leaf_box[i];
             if (A.sh_tex0 >= 0) {
                 int4* tx = reinterpret_cast<int4*>(smem + A.sh_tex0);
                 for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
@@ -2126,7 +2143,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         const uint32_t wi = rel - g * A.fd_rank.d;
                         ck = fdiv(wi, A.fd_tile);
                         it = wi - ck * A.fd_tile.d;
-                        lt = A.tile_perm[g];
+                        lt = A.tile_perm[g];  // (a per-lane cache of it: -0.3 %, profiles/r04/v9_proof_lds_ab.txt)
                         c = lt * A.fd_tile.d + it;
                     } else {  // chunk-major: pass after pass over the slots
                         ck = fdiv(rel, A.fd_total);
@@ -2247,7 +2264,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 #endif
                 if (T.found >= 0) {
                     if (STATS) st.c[ST_NODES]++;  // the leaf-box proof reads one 32-B box record
-                    const float4 ba = w.leaf_box[2 * T.found], bb = w.leaf_box[2 * T.found + 1];
+                    const float4 ba = A.sh_box >= 0 ? smem[A.sh_box + 2 * T.found] : w.leaf_box[2 * T.found];
+                    const float4 bb = A.sh_box >= 0 ? smem[A.sh_box + 2 * T.found + 1] : w.leaf_box[2 * T.found + 1];
 #ifndef RTW_SAH_AUDIT_NO_BOX  // audit builds only: shows that the leaf-box proof decides images
                     ok = ok && box_hit_cond_fast(ba, bb, T.ray, RayPre{T.inv, true}, 0.001f, T.te);
 #else
@@ -3062,6 +3080,8 @@ struct rtw_gpu_world {
     uint32_t order_tiles = 0;
     bool order_valid = false;      // tile permutation computed for order_key
     int32_t last_kernel[4] = {-1, -1, -1, -1};  // LDS mode, leaf kinds, texture kinds, tree of the last render
+    // the last frame: render launches, whole-pixel items, the default threshold, in-frame tuning on
+    int32_t last_frame[4] = {-1, -1, -1, 0};
 };
 
 // experiment builds (-DRTW_WAVE_TIMING): per-wave start / end / queue-empty wall clocks (100 MHz) of
@@ -3494,6 +3514,20 @@ extern "C" RTW_API int rtw_world_kernel(rtw_gpu_world* g, int* lds_mode, int* le
     return RTW_OK;
 }
 
+extern "C" RTW_API int rtw_world_last_frame(rtw_gpu_world* g, int* launches, int* whole_pixel, int* trace_min) {
+    if (!g || !launches || !whole_pixel || !trace_min) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    *launches = g->last_frame[0];
+    *whole_pixel = g->last_frame[1];
+    *trace_min = g->last_frame[2];
+    if (g->last_frame[3]) {  // the kernel takes the world's tuned threshold once there is one
+        HIP_TRY(hipSetDevice(g->device));
+        int v = 0;
+        HIP_TRY(hipMemcpy(&v, &g->tune->chosen, sizeof(int), hipMemcpyDeviceToHost));
+        if (v > 0) *trace_min = v;
+    }
+    return RTW_OK;
+}
+
 extern "C" RTW_API int rtw_world_release(rtw_gpu_world* g) {
     if (!g) return RTW_OK;
     (void)hipSetDevice(g->device);
@@ -3551,7 +3585,7 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.rect_count = g->rect_count;
     A.material_count = g->material_count;
     A.texture_count = g->texture_count;
-    A.sh_li = A.sh_mat = A.sh_tex0 = -1;
+    A.sh_li = A.sh_mat = A.sh_tex0 = A.sh_box = -1;
     A.queue = g->queue;
     A.wdev = g->wdev;
     A.trace_min = 32;
@@ -3624,6 +3658,16 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     A.sh_tex0 = sh && tx == TX_SOLID ? scene_f4 + g->leaf_count + A.material_count : -1;
     A.stack_off = scene_f4 + (sh ? (int32_t)(sh_bytes / sizeof(int4)) : 0);
     if (sh) lds += sh_bytes;
+    // ... and the SAH walk's proof boxes (one read per traced ray, else a dependent L2 read between the
+    // walk and shading; RTW_NO_PROOF_LDS=1 keeps them in HBM / L2)
+    const size_t box_bytes = (size_t)g->leaf_count * 2 * sizeof(float4);
+    const char* npl = std::getenv("RTW_NO_PROOF_LDS");
+    A.sh_box = -1;
+    if (sh && sah && g->w.leaf_box && lds + box_bytes <= cap && !(npl && npl[0] && npl[0] != '0')) {
+        A.sh_box = A.stack_off;
+        A.stack_off += (int32_t)(box_bytes / sizeof(float4));
+        lds += box_bytes;
+    }
     using KFn = void (*)(KArgs);
 #define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}
     static const KFn fns[2][5][3] = {
@@ -3761,6 +3805,9 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
         const char* wp = std::getenv("RTW_WHOLE_PIXEL");
         if (wp && wp[0] == '1') A.whole_pixel = 1;
         else if (!(wp && wp[0] == '0') && (uint64_t)A.total >= env_size("RTW_WHOLE_PIXEL_MIN", 16) * lanes) A.whole_pixel = 1;
+        // its one launch hosts no threshold tuning (the epochs are passes over the slots): a fixed
+        // threshold of 16 (C5: 8 or 16 +0.7 % over 32 and 48, profiles/r04/v9_proof_lds_ab.txt)
+        if (A.whole_pixel && !std::getenv("RTW_TRACE_MIN")) A.trace_min = 16;
     }
     const uint32_t chunk = A.whole_pixel ? A.spp : (uint32_t)std::max<size_t>(1, env_size("RTW_CHUNK", 1));
     // The colour buffer sets the launches per frame (C5, 4K x 2048 spp = 204 GB of colours: 13
@@ -3871,6 +3918,12 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
                                A.total, g->running, s0 == 0 ? 1 : 0, s1 == A.spp ? 1 : 0, A.spp, out, A.layout,
                                A.width, A.height, A.tile_w, A.tile_h, A.tiles_x, A.part_index, A.part_count);
         HIP_TRY(hipGetLastError());
+    }
+    if (!stats) {
+        g->last_frame[0] = launch;
+        g->last_frame[1] = A.whole_pixel ? 1 : 0;
+        g->last_frame[2] = A.trace_min;
+        g->last_frame[3] = A.tune ? 1 : 0;
     }
     if (A.slot_cost && n_tiles_local > 0) {  // the next frame's tile order
         uint32_t* tb = g->tile_buf;

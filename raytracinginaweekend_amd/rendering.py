@@ -132,6 +132,13 @@ class DeviceWorld:
         return {"lds_mode": m.value, "leaf_kinds": lk.value, "tex_kinds": tx.value,
                 "tree": ("reference", "sah")[tr.value] if tr.value >= 0 else None}
 
+    def last_frame(self) -> dict:
+        """The shape of the last frame: render launches, whole-pixel work items (no colour buffer),
+        and the dynamic-fetch threshold it ran with (the tuned one once chosen, else the default)."""
+        n, wp, tm = C.c_int(), C.c_int(), C.c_int()
+        check(lib().rtw_world_last_frame(self._h, C.byref(n), C.byref(wp), C.byref(tm)))
+        return {"launches": n.value, "whole_pixel": bool(wp.value == 1), "trace_min": tm.value}
+
     def collect_stats(self, params: N.RenderParams, tree: int = 0) -> dict:
         """Traversal statistics of one counting-variant render: tree 0 the reference's traversal
         (hittable.rs:429-473), tree 1 the traversal the product kernel runs (the SAH walk, its

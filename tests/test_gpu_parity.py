@@ -428,6 +428,8 @@ def test_whole_pixel_items_bit_exact(worlds, name, parts, monkeypatch):
             fr.launch()
             torch.cuda.synchronize()
             bufs_r = (fr.image if parts == 1 else fr.tiles).cpu().numpy().copy()
+            lf = fr.dworld.last_frame()  # rtw_world_last_frame: one launch of whole-pixel items
+            assert lf["whole_pixel"] and lf["launches"] == 1 and lf["trace_min"] == 16, lf
             if parts == 1:
                 assert_bit_identical(bufs_r.reshape(-1, 3), ref, f"{name} whole-pixel items")
         bufs.append(bufs_r)
