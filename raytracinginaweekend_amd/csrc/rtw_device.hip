@@ -1816,6 +1816,9 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 #ifndef RTW_COOP_PIPE
 #define RTW_COOP_PIPE 1
 #endif
+#ifndef RTW_COOP_TE
+#define RTW_COOP_TE 1
+#endif
 template <int LDS, int LK>
 __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, unsigned long long todo, int32_t n_nodes,
                                         int32_t n_leaves, int32_t n_rects, int32_t fast_off, bool audit) {
@@ -1828,21 +1831,85 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
     const float4* fast = LDS_SCENE ? smem + fast_off : uniform_ptr(w.leaf_fast);
     const int lane = threadIdx.x & 63;
     const uint4* keys = uniform_ptr(w.leaf_key);
-    while (todo) {  // wave-uniform: one ray at a time
-        const int src = __ffsll((long long)todo) - 1;
-        todo &= todo - 1;
+    // one ray's state in the cooperative trace (each lane's best leaf so far, and how many of its
+    // leaves reported exactly that t)
+    struct CRay {
         Ray r;
-        r.o = v3(__shfl(T.ray.o.x, src), __shfl(T.ray.o.y, src), __shfl(T.ray.o.z, src));
-        r.d = v3(__shfl(T.ray.d.x, src), __shfl(T.ray.d.y, src), __shfl(T.ray.d.z, src));
-        r.time = __shfl(T.ray.time, src);
-        const V3 inv = v3(__shfl(T.inv.x, src), __shfl(T.inv.y, src), __shfl(T.inv.z, src));
-        const int32_t sgn = __shfl(T.fast, src);  // bits 0-2: ray.d[axis] > 0
-        float best = F32_INF;
-        int32_t bl = -1;
-        uint32_t cnt = 0;  // leaves of this lane reporting exactly `best`
+        V3 inv;
+        int32_t sgn;  // bits 0-2: ray.d[axis] > 0
+        float best;
+        int32_t bl;
+        uint32_t cnt;
+    };
+    auto load_ray = [&](int src) {
+        CRay c;
+        c.r.o = v3(__shfl(T.ray.o.x, src), __shfl(T.ray.o.y, src), __shfl(T.ray.o.z, src));
+        c.r.d = v3(__shfl(T.ray.d.x, src), __shfl(T.ray.d.y, src), __shfl(T.ray.d.z, src));
+        c.r.time = __shfl(T.ray.time, src);
+        c.inv = v3(__shfl(T.inv.x, src), __shfl(T.inv.y, src), __shfl(T.inv.z, src));
+        c.sgn = __shfl(T.fast, src);
+        c.best = F32_INF;
+        c.bl = -1;
+        c.cnt = 0;
+        return c;
+    };
+    auto keep = [](CRay& c, bool hit, float t, int32_t leaf) {
+        if (hit) {
+            c.cnt = t == c.best ? c.cnt + 1 : t < c.best ? 1u : c.cnt;
+            c.bl = t < c.best ? leaf : c.bl;
+            c.best = t < c.best ? t : c.best;
+        }
+    };
+    // the wave's answer for ray c: the smallest root, its leaf, the tie resolution; written to lane src
+    auto finish = [&](const CRay& c, int src) {
+        float m = c.best;
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) m = rtw_minr(m, __shfl_xor(m, k));
+        const unsigned long long at = __ballot(c.bl >= 0 && c.best == m);
+        bool tie = __ballot(c.bl >= 0 && c.best == m && c.cnt >= 2) != 0;
+        int win = at ? __ffsll((long long)at) - 1 : 0;
+        if (__popcll(at) >= 2) {  // one tied leaf per lane: the first in the reference's DFS order
+            if (keys) {
+                uint32_t k = 0xFFFFFFFFu;
+                if ((at >> lane) & 1) {
+                    const uint4 q = keys[c.bl];
+                    // bit = side XOR (the right child is visited first: ray.d[axis] <= 0)
+                    k = q.x ^ ((c.sgn & 1) ? 0u : q.y) ^ ((c.sgn & 2) ? 0u : q.z) ^ ((c.sgn & 4) ? 0u : q.w);
+                    if (audit) k = ~k;
+                }
+                uint32_t km = k;
+#pragma unroll
+                for (int j = 1; j < 64; j <<= 1) km = min(km, (uint32_t)__shfl_xor((int)km, j));
+                win = __ffsll((long long)__ballot(((at >> lane) & 1) && k == km)) - 1;
+            } else {
+                tie = true;
+            }
+        }
+        const int32_t found = at ? __shfl(c.bl, win) : -1;
+        if (lane == src) {
+            T.found = found;
+            T.te = found >= 0 ? __int_as_float(__float_as_int(m) + 1) : F32_INF;  // succ(t), as take()
+            T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
+            T.sp = 0;
+            T.phase = PH_SHADE;
+        }
+    };
+    // a leaf's first root in [ts, te) with te = succ(the lane's best so far): a root beyond the lane's best
+    // cannot change the lane's answer, and one equal to it still counts (ties); the triangle test then
+    // stops at t for most leaves and reads its record's second half only for closer ones (the drain's
+    // waves read every record of every leaf per ray: LDS-bound)
+    auto te_of = [](const CRay& c) {
+        return RTW_COOP_TE && c.best < F32_INF ? __int_as_float(__float_as_int(c.best) + 1) : F32_INF;
+    };
+    // (two rays per pass over the leaves, sharing the record reads, lost 2.4 % on suzanne and 3.7 % on
+    // cornell_cube to spills: profiles/r04/v10_coop_ab.txt)
+    while (todo) {  // wave-uniform: one ray at a time
+        const int s1 = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        CRay a = load_ray(s1);
         // software-pipelined: the next leaf record is read before this leaf's test, so that its LDS
         // latency overlaps the triangle / rect record read that depends on this one (one round trip per
-        // leaf instead of two; the drain's rays are latency-bound, one at a time per wave)
+        // leaf instead of two; the drain's rays are latency-bound)
 #if RTW_COOP_PIPE
         float4 sph_n = lane < n_leaves ? fast[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #endif
@@ -1854,56 +1921,22 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
             const float4 sph = fast[leaf];
 #endif
             float t;
-            bool hit;
+            const float te = te_of(a);
             if (LK == LK_SPHERES || sph.w == sph.w) {
-                hit = sphere_t(sph, r, 0.001f, F32_INF, t);
+                keep(a, sphere_t(sph, a.r, 0.001f, te, t), t, leaf);
             } else if (LK >= LK_PLAIN && __float_as_int(sph.x) == 2) {
                 const int ri = __float_as_int(sph.y);
                 const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
                 const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
-                hit = rect_t_mk(g, r, inv, 0.001f, F32_INF, t);  // SAH rays are Markstein-exact
+                keep(a, rect_t_mk(g, a.r, a.inv, 0.001f, te, t), t, leaf);  // SAH rays are Markstein-exact
             } else {
                 const int ti = __float_as_int(sph.y);
-                hit = tri_test(LDS == 2 ? load_tri_soa(tri_fast, RTW_TRI_BY_LEAF ? leaf : ti) : load_tri(tri_fast, ti), r, 0.001f,
-                               F32_INF, t);
-            }
-            if (hit) {
-                cnt = t == best ? cnt + 1 : t < best ? 1u : cnt;
-                bl = t < best ? leaf : bl;
-                best = t < best ? t : best;
+                keep(a, tri_test(LDS == 2 ? load_tri_soa(tri_fast, RTW_TRI_BY_LEAF ? leaf : ti) : load_tri(tri_fast, ti), a.r,
+                                 0.001f, te, t),
+                     t, leaf);
             }
         }
-        float m = best;
-#pragma unroll
-        for (int k = 1; k < 64; k <<= 1) m = rtw_minr(m, __shfl_xor(m, k));
-        const unsigned long long at = __ballot(bl >= 0 && best == m);
-        bool tie = __ballot(bl >= 0 && best == m && cnt >= 2) != 0;
-        int win = at ? __ffsll((long long)at) - 1 : 0;
-        if (__popcll(at) >= 2) {  // one tied leaf per lane: the first in the reference's DFS order
-            if (keys) {
-                uint32_t k = 0xFFFFFFFFu;
-                if ((at >> lane) & 1) {
-                    const uint4 q = keys[bl];
-                    // bit = side XOR (the right child is visited first: ray.d[axis] <= 0)
-                    k = q.x ^ ((sgn & 1) ? 0u : q.y) ^ ((sgn & 2) ? 0u : q.z) ^ ((sgn & 4) ? 0u : q.w);
-                    if (audit) k = ~k;
-                }
-                uint32_t km = k;
-#pragma unroll
-                for (int j = 1; j < 64; j <<= 1) km = min(km, (uint32_t)__shfl_xor((int)km, j));
-                win = __ffsll((long long)__ballot(((at >> lane) & 1) && k == km)) - 1;
-            } else {
-                tie = true;
-            }
-        }
-        const int32_t found = at ? __shfl(bl, win) : -1;
-        if (lane == src) {
-            T.found = found;
-            T.te = found >= 0 ? __int_as_float(__float_as_int(m) + 1) : F32_INF;  // succ(t), as take()
-            T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
-            T.sp = 0;
-            T.phase = PH_SHADE;
-        }
+        finish(a, s1);
     }
     return T;
 }
