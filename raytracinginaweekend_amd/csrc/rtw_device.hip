@@ -1683,7 +1683,10 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         // wall rects, ~0.8: -8 %), hence only for worlds without rect, box or wrapped leaves.
         // The two-children step of plain-sphere SAH walks (C2) halves the node steps between leaves:
         // there a leaf body on every step is 3 % faster (profiles/r02/v9_leaf_cadence_ab.txt).
-        if (!C2_INLINE && (STATS || C2 || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
+#ifndef RTW_LEAF_CADENCE
+#define RTW_LEAF_CADENCE 2  // leaf bodies on every RTW_LEAF_CADENCE-th step (sphere / triangle worlds)
+#endif
+        if (!C2_INLINE && (STATS || C2 || u % RTW_LEAF_CADENCE == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
             test_leaf(-1 - T.node);
             pop();
         }
