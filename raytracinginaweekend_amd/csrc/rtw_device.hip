@@ -3749,7 +3749,8 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     A.tune_items = 0;
     if (A.tune && A.total > 0 && !A.tile_perm) {  // epochs are whole passes: chunk-major order only
         const uint64_t lanes = (uint64_t)blocks * RTW_BLOCK;
-        const uint64_t E = (uint64_t)A.total * ((2 * lanes + A.total - 1) / A.total);
+        const uint64_t lx = env_size("RTW_TUNE_LANES_X", 2);  // epoch length: at least lx x the resident lanes
+        const uint64_t E = (uint64_t)A.total * ((lx * lanes + A.total - 1) / A.total);
         if (A.items_big >= (uint64_t)(RTW_TUNE_EPOCHS + 2) * E) {
             A.tune_items = E;
             HIP_TRY(hipMemsetAsync(A.tune->tb, 0xFF, sizeof(A.tune->tb), stream));
