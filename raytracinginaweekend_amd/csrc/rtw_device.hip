@@ -1554,6 +1554,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             T.found = leaf;
         }
     };
+    // (take() under the hit predicate as selects, with no branch around it in the two-children step:
+    // -0.8 %, profiles/r04/v19_take_sel_ab.txt)
     // SAH walk of plain-sphere worlds: two children per node step (below).  (Stack entries packing
     // the pushed child's entry t, so that a pop skips children starting beyond te, lost 5 %: the
     // skip loop's divergence costs more than the node steps it saves, profiles/r02/v9_two_child_ab.txt.)
