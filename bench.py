@@ -366,6 +366,49 @@ def launch_ranks(args) -> int:
     return rc
 
 
+def inproc_bench(args) -> int:
+    """--inproc: the N GPUs from one process through the C ABI's multi-device path (rtw_multi_create /
+    rtw_multi_render: one host thread and stream per device, the tile buffers peer-copied to GPU 0 over
+    xGMI, untiled there), the way a single caller of rendering::render (main.rs:43-50) takes the node.
+    A timed frame is the whole rtw_multi_render call: every partition's render, the copies, the untile."""
+    devices = [int(x) for x in args.inproc_devices.split(",")] if args.inproc_devices else list(range(args.gpus))
+    if not args.inproc_devices and count_gpus() < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs", file=sys.stderr)
+        return 3
+    import torch
+
+    import raytracinginaweekend_amd as R
+
+    world = R.demo_world(args.scene)
+    size = R.Size2i(args.width, args.height)
+    p = R.render_params(size, args.spp, args.max_depth, seed=args.seed, part=(0, 0))
+    mw = R.MultiDeviceWorld(world, devices)
+    img = torch.empty(size.count() * 3, dtype=torch.float32, device=f"cuda:{devices[0]}")
+    for _ in range(args.warmup):
+        mw.render_into(p, img.data_ptr())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mw.render_into(p, img.data_ptr())
+    elapsed = time.perf_counter() - t0
+    if args.save:
+        from raytracinginaweekend_amd.image_io import save_image
+
+        save_image(args.save, img.cpu().numpy().reshape(-1, 3), args.width, args.height)
+    value = args.width * args.height * args.spp * args.steps / elapsed / 1e6
+    print(json.dumps({
+        "metric": "Msamples/sec at 1920x1080x512spp; achieved HBM GB/s vs peak",
+        "value": round(value, 3), "unit": "Msamples/sec", "n_gpus": len(set(devices)), "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": f"synthetic: the reference's demo world {args.scene}, built as its builder does from fixed seeds",
+        "config": {"workload": f"{args.scene} {args.width}x{args.height}x{args.spp}spp max_depth {args.max_depth}",
+                   "parallelism": f"in-process: {len(devices)} partitions on devices {devices} (rtw_multi_render: "
+                                  "one host thread per partition, peer copies to the first device, untile)"},
+    }), flush=True)
+    mw.release()
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -391,7 +434,13 @@ def main() -> int:
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--save", default="", help="write the rank-0 image (.ppm/.png)")
+    ap.add_argument("--inproc", action="store_true",
+                    help="one process drives the --gpus devices through rtw_multi_render (no ranks, no RCCL)")
+    ap.add_argument("--inproc-devices", default="", help="with --inproc: an explicit device list, e.g. 0,0,0")
     args = ap.parse_args()
+
+    if args.inproc:
+        return inproc_bench(args)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args)
@@ -567,6 +616,7 @@ def main() -> int:
         save_image(args.save, fr.image.cpu().numpy().reshape(-1, 3), args.width, args.height)
 
     if rank == 0:
+        last = fr.dworld.last_frame()
         line = {
             "metric": "Msamples/sec at 1920x1080x512spp; achieved HBM GB/s vs peak",
             "value": round(value, 3),
@@ -589,10 +639,10 @@ def main() -> int:
                 "max_depth": args.max_depth,
                 "partition": f"interleaved {spec.tile[0]}x{spec.tile[1]} tiles over {world_size} GPU(s)",
                 "rccl_world_size": world_size,
-                "trace_min": fr.dworld.last_frame()["trace_min"],
+                "trace_min": last["trace_min"],
                 "kernel": fr.dworld.kernel_variant(),
-                "launches_per_frame": fr.dworld.last_frame()["launches"],
-                "work_items": "whole pixels" if fr.dworld.last_frame()["whole_pixel"] else "samples",
+                "launches_per_frame": last["launches"],
+                "work_items": None if last["whole_pixel"] is None else "whole pixels" if last["whole_pixel"] else "samples",
             },
             "first_frame_ms": first_frame_ms,
             "first_frame_Msamples_s": round(args.width * args.height * args.spp / first_frame_ms / 1e3, 1)

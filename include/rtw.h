@@ -256,6 +256,23 @@ typedef void (*rtw_progress_fn)(uint64_t done_samples, uint64_t total_samples, v
 RTW_API int rtw_render_progress(const rtw_world* world, const rtw_render_params* params, int device,
                                 float* out_rgb, rtw_progress_fn cb, void* user);
 
+/* rtw_render on several GPUs of one node (one call may use several devices).  The
+ * frame's interleaved tile_width x tile_height tiles (params->tile_*, default 8x8) are split over the
+ * list: entry i renders the tiles t with t % n_devices == i on devices[i], on its own host thread; the
+ * tile buffers reach devices[0] by peer copy over xGMI and are placed there (rtw_untile_device); the
+ * image is copied into host `out_rgb` as rtw_render does.  A device may repeat (several partitions on
+ * one GPU).  Bit-identical to rtw_render for every list (per-(pixel, sample) RNG streams).
+ * params->part_index / part_count must be 0 / 0 or 1: the call partitions the frame itself. */
+RTW_API int rtw_render_devices(const rtw_world* world, const rtw_render_params* params, const int* devices,
+                               int n_devices, float* out_rgb);
+/* The same, resident: rtw_multi_create uploads the world to every listed device once;
+ * rtw_multi_render renders one frame and leaves the W*H*3 f32 image in d_image on devices[0]
+ * (synchronous: it returns when the image is complete). */
+typedef struct rtw_multi rtw_multi;
+RTW_API int rtw_multi_create(const rtw_world* world, const int* devices, int n_devices, rtw_multi** out);
+RTW_API int rtw_multi_render(rtw_multi* m, const rtw_render_params* params, float* d_image);
+RTW_API int rtw_multi_release(rtw_multi* m);
+
 /* Resident path: upload once, render many times into device memory. */
 RTW_API int rtw_world_upload(const rtw_world* world, int device, rtw_gpu_world** out);
 RTW_API int rtw_world_release(rtw_gpu_world* gw);

@@ -234,6 +234,9 @@ extern "C" {
     pub fn rtw_render(world: *const RtwWorld, params: *const RtwRenderParams, device: c_int, out_rgb: *mut f32) -> c_int;
     pub fn rtw_render_progress(world: *const RtwWorld, params: *const RtwRenderParams, device: c_int, out_rgb: *mut f32,
                                cb: Option<RtwProgressFn>, user: *mut c_void) -> c_int;
+    pub fn rtw_render_devices(world: *const RtwWorld, params: *const RtwRenderParams, devices: *const c_int,
+                              n_devices: c_int, out_rgb: *mut f32) -> c_int;
+    pub fn rtw_device_count(count: *mut c_int) -> c_int;
 }
 
 fn check(rc: c_int, what: &str) {
@@ -553,12 +556,11 @@ pub fn render_gpu(image_size: Size2i, thread_count: usize, samples_per_pixel: us
     render_gpu_seeded(image_size, thread_count, samples_per_pixel, max_depth, world, render_mode, seed, 0)
 }
 
-pub fn render_gpu_seeded(image_size: Size2i, thread_count: usize, samples_per_pixel: usize, max_depth: i32,
-                         world: &World, render_mode: RenderMode, seed: u64, device: i32) -> Vec<Color> {
+fn params(image_size: Size2i, thread_count: usize, samples_per_pixel: usize, max_depth: i32, render_mode: RenderMode,
+          seed: u64) -> RtwRenderParams {
     assert_eq!(unsafe { rtw_version() }, RTW_ABI_VERSION, "librtw.so ABI version mismatch");
     assert!(thread_count >= 1, "attempt to divide by zero"); // split_work_tasks (rendering.rs:223)
-    let (f, w) = serialise(world);
-    let p = RtwRenderParams {
+    RtwRenderParams {
         width: image_size.width,
         height: image_size.height,
         samples_per_pixel: u32::try_from(samples_per_pixel).expect("samples_per_pixel exceeds u32::MAX"),
@@ -575,7 +577,17 @@ pub fn render_gpu_seeded(image_size: Size2i, thread_count: usize, samples_per_pi
         part_count: 1,
         thread_count: thread_count.min(i32::MAX as usize) as i32,
         reserved0: 0,
-    };
+    }
+}
+
+fn colors(out: Vec<f32>) -> Vec<Color> {
+    out.chunks_exact(3).map(|c| Color::new_rgb(c[0], c[1], c[2])).collect()
+}
+
+pub fn render_gpu_seeded(image_size: Size2i, thread_count: usize, samples_per_pixel: usize, max_depth: i32,
+                         world: &World, render_mode: RenderMode, seed: u64, device: i32) -> Vec<Color> {
+    let p = params(image_size, thread_count, samples_per_pixel, max_depth, render_mode, seed);
+    let (f, w) = serialise(world);
     let n = (image_size.width as usize) * (image_size.height as usize);
     let mut out = vec![0f32; n * 3];
     eprintln!("Start rendering...");
@@ -584,5 +596,31 @@ pub fn render_gpu_seeded(image_size: Size2i, thread_count: usize, samples_per_pi
     check(rc, "rtw_render_progress");
     eprintln!("\rRendering done in {} seconds", start.elapsed().as_secs_f64());
     drop(f);
-    out.chunks_exact(3).map(|c| Color::new_rgb(c[0], c[1], c[2])).collect()
+    colors(out)
+}
+
+/// rendering::render on every GPU of the node (the reference's `render` uses every core,
+/// main.rs:19): the interleaved tiles are split over `devices`, rendered in parallel, gathered on
+/// devices[0] over xGMI (rtw_render_devices).  Bit-identical to `render_gpu_seeded` with the same
+/// seed for every device list.  An empty list means all devices.
+pub fn render_gpu_devices(image_size: Size2i, thread_count: usize, samples_per_pixel: usize, max_depth: i32,
+                          world: &World, render_mode: RenderMode, seed: u64, devices: &[i32]) -> Vec<Color> {
+    let p = params(image_size, thread_count, samples_per_pixel, max_depth, render_mode, seed);
+    let all: Vec<c_int> = if devices.is_empty() {
+        let mut n: c_int = 0;
+        check(unsafe { rtw_device_count(&mut n) }, "rtw_device_count");
+        (0..n.max(1)).collect()
+    } else {
+        devices.iter().map(|&d| d as c_int).collect()
+    };
+    let (f, w) = serialise(world);
+    let n = (image_size.width as usize) * (image_size.height as usize);
+    let mut out = vec![0f32; n * 3];
+    eprintln!("Start rendering on {} GPU(s)...", all.len());
+    let start = std::time::Instant::now();
+    let rc = unsafe { rtw_render_devices(&w, &p, all.as_ptr(), all.len() as c_int, out.as_mut_ptr()) };
+    check(rc, "rtw_render_devices");
+    eprintln!("Rendering done in {} seconds", start.elapsed().as_secs_f64());
+    drop(f);
+    colors(out)
 }

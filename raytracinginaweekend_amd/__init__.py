@@ -6,7 +6,16 @@ include/rtw.h).  This package is its Python face, mirroring the reference's inte
 Camera.build()..., WorldBuilder / NodeBuilder, demo worlds, rendering.render(...).
 """
 from . import image_io
-from .rendering import DeviceWorld, RenderMode, Size2i, device_count, render, render_params
+from .rendering import (
+    DeviceWorld,
+    MultiDeviceWorld,
+    RenderMode,
+    Size2i,
+    device_count,
+    render,
+    render_devices,
+    render_params,
+)
 from .world import (
     DEMO_WORLDS,
     AssetSet,
@@ -27,6 +36,7 @@ __all__ = [
     "Camera",
     "DEMO_WORLDS",
     "DeviceWorld",
+    "MultiDeviceWorld",
     "NodeBuilder",
     "NodeRef",
     "RenderMode",
@@ -38,5 +48,6 @@ __all__ = [
     "device_count",
     "load_obj_mesh",
     "render",
+    "render_devices",
     "render_params",
 ]

@@ -61,12 +61,9 @@
 #ifndef RTW_QUEUES
 #define RTW_QUEUES 16
 #endif
-#ifndef RTW_PREFETCH
-// 1: fetch a wave's next batch one refill ahead.  Measured slower (final_scene1 -3 %, suzanne -9 %,
-// profiles/r03/v1_queue_ab.txt): the pending atomic holds back the wave's next vector-memory waits
-// and a wave holds two batches; so the batch is fetched when the reserve runs out
-#define RTW_PREFETCH 0
-#endif
+// (Fetching a wave's next batch one refill ahead was slower -- final_scene1 -3 %, suzanne -9 %,
+// profiles/r03/v1_queue_ab.txt: the pending atomic holds back the wave's next vector-memory waits and a
+// wave holds two batches -- so the batch is fetched when the reserve runs out.)
 #define RTW_QGRAN 64
 #define RTW_QSTRIDE 32  // u64 counters per queue slot (256 B)
 // a frame's launch l takes its items from queue block min(l, RTW_QUEUE_SLOTS - 1) of the world's
@@ -394,12 +391,8 @@ __device__ __forceinline__ uint64_t d_rotl64(uint64_t x, int k) {  // k: a const
     }
     return ((uint64_t)nhi << 32) | nlo;
 }
-// (RTW_DEV_RNG=0 builds draw through rtw_scalar.h's functions instead: the A/B baseline)
-#ifndef RTW_DEV_RNG
-#define RTW_DEV_RNG 1
-#endif
+// (Against drawing through rtw_scalar.h's functions: final_scene1 +2.8 %, profiles/r04/v8_device_rng_ab.txt.)
 __device__ __forceinline__ uint64_t d_next_u64(rtw_xoro* r) {  // rtw_xoro_next_u64
-    if (!RTW_DEV_RNG) return rtw_xoro_next_u64(r);
     const uint64_t s0 = r->s0;
     uint64_t s1 = r->s1;
     const uint64_t result = d_rotl64(s0 + s1, 17) + s0;
@@ -410,11 +403,9 @@ __device__ __forceinline__ uint64_t d_next_u64(rtw_xoro* r) {  // rtw_xoro_next_
 }
 __device__ __forceinline__ uint32_t d_next_u32(rtw_xoro* r) { return (uint32_t)d_next_u64(r); }
 __device__ __forceinline__ float d_value0_1(uint32_t u) {
-    if (!RTW_DEV_RNG) return rtw_value0_1(u);
     return __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, u, 9)) - 1.0f;
 }
 __device__ __forceinline__ float d_m1_1(rtw_xoro* r) {  // rtw_uniform_m1_1
-    if (!RTW_DEV_RNG) return rtw_uniform_m1_1(r);
     return __uint_as_float(__builtin_amdgcn_alignbit(0x80u, d_next_u32(r), 9)) - 3.0f;
 }
 __device__ __forceinline__ float d_gen_f32(rtw_xoro* r) {  // rtw_gen_f32
@@ -446,7 +437,7 @@ __device__ __forceinline__ V3 d_unit_sphere(rtw_xoro* r) {  // rtw_unit_sphere
         sum = x1 * x1 + x2 * x2;
         if (sum < 1.0f) break;
     }
-    const float factor = 2.0f * (RTW_DEV_RNG ? sqrt_nr(1.0f - sum) : __builtin_sqrtf(1.0f - sum));
+    const float factor = 2.0f * sqrt_nr(1.0f - sum);
     return v3(x1 * factor, x2 * factor, 1.0f - 2.0f * sum);
 }
 __device__ __forceinline__ V3 d_unit_ball(rtw_xoro* r) {  // rtw_unit_ball
@@ -659,12 +650,9 @@ __device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i
 #ifndef RTW_TRI_SOA
 #define RTW_TRI_SOA 1024
 #endif
-// RTW_TRI_BY_LEAF=1 builds index them by leaf instead and load a leaf's record with its leaf record,
-// before knowing it is a triangle: one dependent LDS read less per triangle test, but suzanne -1.8 %
-// (the early record's 16 VGPRs; profiles/r04/v5_experiments_ab.txt)
-#ifndef RTW_TRI_BY_LEAF
-#define RTW_TRI_BY_LEAF 0
-#endif
+// (Indexing them by leaf instead, and loading a leaf's record with its leaf record before knowing it is a
+// triangle -- one dependent LDS read less per triangle test -- lost 1.8 % on suzanne: the early record's
+// 16 VGPRs; profiles/r04/v5_experiments_ab.txt.)
 __device__ __forceinline__ TriFast load_tri_soa(const float4* __restrict__ tf, int i) {
     const float4 a = tf[i], b = tf[RTW_TRI_SOA + i], c = tf[2 * RTW_TRI_SOA + i], d = tf[3 * RTW_TRI_SOA + i];
     TriFast f;
@@ -693,43 +681,22 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
     return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 // the per-ray part; barycentrics are recomputed from (ray, t) by leaf_record
-#ifdef RTW_EXP_FASTDIV_TRI  // experiment builds only (inexact: wrong images): the cost of the divisions
-#define RTW_TDIV(a, b) ((a) * __builtin_amdgcn_rcpf(b))
-#else
-#define RTW_TDIV(a, b) ((a) / (b))
-#endif
-// t = num / denom without the division sequence (RTW_TRI_T_MK): with 1e-4 < |denom| <= |d||n| ~ 1 the
+// t = num / denom without the division sequence: with 1e-4 < |denom| <= |d||n| ~ 1 the
 // divisor is inside Markstein's guard; a dividend outside its guard is 0 or below 2^-80
 // (then both quotients lie below ts = 0.001: the test fails either way) -- the upper bound holds as
 // coordinates are below 2^30.  So the quotient decides contains(ts, te, t) as RN(num / denom) does and
-// equals it whenever that passes: no guard, no branch (rtw_device_check_division test 5).
-#ifndef RTW_TRI_T_MK
-#define RTW_TRI_T_MK 1  // suzanne +1.4 %, cornell_cube +1.7 % (profiles/r04/v2_experiments_ab.txt)
-#endif
+// equals it whenever that passes: no guard, no branch (rtw_device_check_division test 5).  Against the
+// IEEE division: suzanne +1.4 %, cornell_cube +1.7 % (profiles/r04/v2_experiments_ab.txt).
 __device__ __forceinline__ float tri_t_mk(float num, float denom) { return mk_corr(num, denom, rcp_nr(denom)); }
 __device__ __forceinline__ bool tri_test(const TriFast& T, const Ray& r, float ts, float te, float& t) {
     const float denom = dot(r.d, T.n);
     if (!(__builtin_fabsf(denom) > 0.0001f)) return false;
-    // t keeps the IEEE division unless RTW_TRI_T_MK: rcp_nr + the correction + a dividend guard cost
-    // suzanne 3 % against it (register pressure in the leaf body; profiles/r03/v5_division_ab.txt)
-#if RTW_TRI_T_MK && !defined(RTW_EXP_FASTDIV_TRI)
     t = tri_t_mk(dot(sub(T.p0, r.o), T.n), denom);
-#else
-    t = RTW_TDIV(dot(sub(T.p0, r.o), T.n), denom);
-#endif
     if (!contains(ts, te, t)) return false;
     const V3 q = sub(at(r, t), T.p0);
-#ifdef RTW_EXP_FASTDIV_TRI
-    const float w1 = RTW_TDIV(dot(q, T.vt1), T.den1);
-#else
     const float w1 = div_tri(dot(q, T.vt1), T.den1, T.y1);
-#endif
     if (!(w1 > 0.0f && w1 < 1.0f)) return false;
-#ifdef RTW_EXP_FASTDIV_TRI
-    const float w2 = RTW_TDIV(dot(q, T.vt2), T.den2);
-#else
     const float w2 = div_tri(dot(q, T.vt2), T.den2, T.y2);
-#endif
     const float w0 = 1.0f - w1 - w2;
     return w2 > 0.0f && w0 > 0.0f;
 }
@@ -1079,15 +1046,9 @@ __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, 
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
     const float delta = sah_delta<DQ>(km.x, km.y, a0, b0, a1, b1, a2, b2);
-#ifdef RTW_SAH_EXACT_Q  // audit / A/B builds: the exact quotients of the reference tree's test
-    const float qa0 = mk_div(a0, r.d.x, rp.inv.x), qb0 = mk_div(b0, r.d.x, rp.inv.x);
-    const float qa1 = mk_div(a1, r.d.y, rp.inv.y), qb1 = mk_div(b1, r.d.y, rp.inv.y);
-    const float qa2 = mk_div(a2, r.d.z, rp.inv.z), qb2 = mk_div(b2, r.d.z, rp.inv.z);
-#else
     const float qa0 = a0 * rp.inv.x, qb0 = b0 * rp.inv.x;
     const float qa1 = a1 * rp.inv.y, qb1 = b1 * rp.inv.y;
     const float qa2 = a2 * rp.inv.z, qb2 = b2 * rp.inv.z;
-#endif
     const float w0 = delta * __builtin_fabsf(rp.inv.x), w1 = delta * __builtin_fabsf(rp.inv.y),
                 w2 = delta * __builtin_fabsf(rp.inv.z);
     const float lo = __builtin_fmaxf(
@@ -1543,12 +1504,17 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // DFS order) is seen and flagged
     auto take = [&](float t, int leaf) {
         if (TM == TM_SAH) {
-            // selects, not branches (+1.6 % on final_scene1: the branchy form cost exec-mask work)
-            // (a leaf referenced twice -- a spatial split of the SAH tree, rtw_sah.cpp -- meets itself: no tie)
-            const bool tie = T.found >= 0 && T.found != leaf && t == __int_as_float(__float_as_int(T.te) - 1);
-            T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
-            T.te = tie ? T.te : __int_as_float(__float_as_int(t) + 1);  // t >= 0.001: the next float up
-            T.found = tie ? T.found : leaf;
+            // selects, not branches (+1.6 % on final_scene1: the branchy form cost exec-mask work).
+            // t < te = succ(closest), so t is either the closest t again (`same`) or strictly closer.
+            // Strictly closer: a new closest leaf, any earlier tie is void.  The same t from another
+            // leaf: a tie.  The same t from the kept leaf itself (a leaf referenced twice -- a spatial
+            // split of the SAH tree, rtw_sah.cpp): nothing changes, and a tie flagged by a third leaf
+            // in between must stay (clearing it there let the proof pass without a re-trace)
+            const bool same = T.found >= 0 && t == __int_as_float(__float_as_int(T.te) - 1);
+            const bool tie = same && T.found != leaf;
+            T.fast = same ? (tie ? (T.fast | RTW_TF_TIE) : T.fast) : (T.fast & ~RTW_TF_TIE);
+            T.te = same ? T.te : __int_as_float(__float_as_int(t) + 1);  // t >= 0.001: the next float up
+            T.found = same ? T.found : leaf;
         } else {
             T.te = t;
             T.found = leaf;
@@ -1559,32 +1525,20 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // SAH walk of plain-sphere worlds: two children per node step (below).  (Stack entries packing
     // the pushed child's entry t, so that a pop skips children starting beyond te, lost 5 %: the
     // skip loop's divergence costs more than the node steps it saves, profiles/r02/v9_two_child_ab.txt.)
+    // The two-children step tests a leaf child's sphere at once: leaves are never pushed or stood on, so
+    // the loop has no leaf steps (final_scene1 +3.0 % over round 2's leaf-then-node step,
+    // profiles/r03/v9_inline_leaf_ab.txt).  The lane carries, instead of the node it stands on, that
+    // node's two children packed in 16 bits each: they came with the node's box record in its parent's
+    // step (nodes_b.zw), and a pushed node is pushed as its children -- one dependent LDS read less per
+    // step (+0.9 %, profiles/r04/v4_experiments_ab.txt; worlds of < 2^15 nodes and leaves, checked at
+    // upload).
     constexpr bool C2 = TM == TM_SAH && LK == LK_SPHERES;
-#ifndef RTW_C2_INLINE
-#define RTW_C2_INLINE 1
-#endif
-    // the two-children step tests a leaf child's sphere at once: leaves are never pushed or stood on,
-    // so the loop has no leaf steps (final_scene1 +3.0 %, profiles/r03/v9_inline_leaf_ab.txt;
-    // RTW_C2_INLINE=0 builds keep round 2's leaf-then-node step)
-    constexpr bool C2_INLINE = C2 && RTW_C2_INLINE;
-    // ... and carries, instead of the node it stands on, that node's two children packed in 16 bits each
-    // (C2P): they came with the node's box record in its parent's step (nodes_b.zw), and a pushed node
-    // is pushed as its children -- one dependent LDS read less per step (worlds of < 2^15 nodes and
-    // leaves, checked at upload; RTW_C2_PACKED=0 builds read the children from the node)
-#ifndef RTW_C2_PACKED
-#define RTW_C2_PACKED 1
-#endif
-    constexpr bool C2P = C2_INLINE && RTW_C2_PACKED;
     auto pack2 = [](float4 nb) {  // {.., .., bits(left << 2 | axis), bits(right)} -> left | right << 16
         return (int32_t)(((uint32_t)(__float_as_int(nb.z) >> 2) & 0xFFFFu) | ((uint32_t)__float_as_int(nb.w) << 16));
     };
-    // the SAH node test's k term: D^2 (two operations; every world gained 0.5 %,
-    // profiles/r03/v6_delta_d2_ab.txt); RTW_SAH_DQ builds keep round 2's Dq form
-#ifdef RTW_SAH_DQ
-    constexpr bool SAH_DQ = true;
-#else
+    // the SAH node test's k term: D^2 (two operations; every world gained 0.5 % over round 2's Dq form,
+    // profiles/r03/v6_delta_d2_ab.txt)
     constexpr bool SAH_DQ = false;
-#endif
     // (reading the stack's top as each step starts, so that a pop finds it arrived, lost 0.4-2.3 %:
     // profiles/r04/v6_spec_pop_ab.txt)
     auto pop = [&]() {
@@ -1598,11 +1552,6 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // one leaf's test at the current t range (hittable.rs:436-437: a leaf is never box-tested)
     auto test_leaf = [&](int leaf) {
         const float4 sph = fast[leaf];
-        // mode 2 with leaf-indexed triangle records: load the record with the leaf record, before the
-        // leaf's kind is known (a sphere or rect leaf reads an unused slot)
-        constexpr bool TRI_EARLY = RTW_TRI_BY_LEAF && LDS == 2 && LDS_SCENE && (LK == LK_TRIS || LK == LK_PLAIN);
-        TriFast tfe;
-        if (TRI_EARLY) tfe = load_tri_soa(tri_fast, leaf);
         if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
             if (STATS) st.c[ST_T_SPHERE]++;
             float t;
@@ -1620,9 +1569,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             if (STATS) st.c[ST_T_TRI]++;
             float t;
             const int ti = __float_as_int(sph.y);
-            if (tri_test(TRI_EARLY ? tfe : LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, RTW_TRI_BY_LEAF ? leaf : ti)
-                                                 : load_tri(tri_fast, ti),
-                         T.ray, 0.001f, T.te, t))
+            if (tri_test(LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), T.ray, 0.001f,
+                         T.te, t))
                 take(t, leaf);
         } else if (LK >= LK_WRAPPED) {
             float t;
@@ -1685,10 +1633,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
         // wall rects, ~0.8: -8 %), hence only for worlds without rect, box or wrapped leaves.
         // The two-children step of plain-sphere SAH walks (C2) halves the node steps between leaves:
         // there a leaf body on every step is 3 % faster (profiles/r02/v9_leaf_cadence_ab.txt).
-#ifndef RTW_LEAF_CADENCE
-#define RTW_LEAF_CADENCE 2  // leaf bodies on every RTW_LEAF_CADENCE-th step (sphere / triangle worlds)
-#endif
-        if (!C2_INLINE && (STATS || C2 || u % RTW_LEAF_CADENCE == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
+        // (every third step instead: suzanne -8.6 %, profiles/r04/v16_leaf_cadence_ab.txt)
+        if (!C2 && (STATS || u % 2 == 0 || LK >= LK_PLAIN) && T.phase == ACT && T.node < 0) {
             test_leaf(-1 - T.node);
             pop();
         }
@@ -1699,58 +1645,37 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 db[DB_NODE_LANES] += (uint32_t)__popcll(nm);
             }
         }
-#ifndef RTW_SAH_ONE_CHILD
-        if (C2 && T.phase == ACT && (C2P || T.node >= 0)) {
+        if (C2 && T.phase == ACT) {
             // SAH walk, two children per step: the lane stands on a node already accepted (the root,
             // or a child accepted by its parent's step) and tests both children's grown boxes at once
             // (leaf children need no box: their own test follows); accepted children are visited
             // near first (a leaf first), the other one pushed.  Any visit order finds the same
             // closest root (§5.5 step 1), so only the work changes.
-            int32_t left, right;
-            if (C2P) {
-                left = (int32_t)(int16_t)(T.node & 0xFFFF);
-                right = T.node >> 16;
+            const int32_t left = (int32_t)(int16_t)(T.node & 0xFFFF);
+            const int32_t right = T.node >> 16;
+            float el = F32_INF, er = F32_INF;
+            bool pl = false, pr = false;
+            int32_t lc = left, rc = right;  // what stands for an accepted child: its packed children
+            // leaf children: their sphere now (never pushed or visited); internal ones: the box
+            if (left < 0) {
+                if (STATS) st.c[ST_T_SPHERE]++;
+                float t;
+                if (sphere_t(fast[-1 - left], T.ray, 0.001f, T.te, t)) take(t, -1 - left);
             } else {
-                const float2 ch = reinterpret_cast<const float2*>(nodes_b)[2 * T.node + 1];
-                left = __float_as_int(ch.x) >> 2;
-                right = __float_as_int(ch.y);
+                if (STATS) st.c[ST_NODES]++;
+                const float4 nb = nodes_b[left];
+                pl = node_pass_cons<SAH_DQ>(nodes_a[left], nb, nkm[left], T.ray, rp, 0.001f, T.te, el);
+                lc = pack2(nb);
             }
-            const int32_t il = left >= 0 ? left : 0, ir = right >= 0 ? right : 0;
-            float el, er;
-            bool pl, pr;
-            int32_t lc = left, rc = right;  // what stands for an accepted child: C2P its children, else itself
-            if (C2_INLINE) {
-                // leaf children: their sphere now (never pushed or visited); internal ones: the box
-                pl = pr = false;
-                el = er = F32_INF;
-                if (left < 0) {
-                    if (STATS) st.c[ST_T_SPHERE]++;
-                    float t;
-                    if (sphere_t(fast[-1 - left], T.ray, 0.001f, T.te, t)) take(t, -1 - left);
-                } else {
-                    if (STATS) st.c[ST_NODES]++;
-                    const float4 nb = nodes_b[left];
-                    pl = node_pass_cons<SAH_DQ>(nodes_a[left], nb, nkm[left], T.ray, rp, 0.001f, T.te, el);
-                    if (C2P) lc = pack2(nb);
-                }
-                if (right < 0) {
-                    if (STATS) st.c[ST_T_SPHERE]++;
-                    float t;
-                    if (sphere_t(fast[-1 - right], T.ray, 0.001f, T.te, t)) take(t, -1 - right);
-                } else {
-                    if (STATS) st.c[ST_NODES]++;
-                    const float4 nb = nodes_b[right];
-                    pr = node_pass_cons<SAH_DQ>(nodes_a[right], nb, nkm[right], T.ray, rp, 0.001f, T.te, er);
-                    if (C2P) rc = pack2(nb);
-                }
+            if (right < 0) {
+                if (STATS) st.c[ST_T_SPHERE]++;
+                float t;
+                if (sphere_t(fast[-1 - right], T.ray, 0.001f, T.te, t)) take(t, -1 - right);
             } else {
-                const float4 la = nodes_a[il], lb = nodes_b[il], ra = nodes_a[ir], rb = nodes_b[ir];
-                const float2 lk = nkm[il], rk = nkm[ir];
-                if (STATS) st.c[ST_NODES] += (left >= 0) + (right >= 0);  // the child boxes tested
-                pl = node_pass_cons<SAH_DQ>(la, lb, lk, T.ray, rp, 0.001f, T.te, el) || left < 0;
-                pr = node_pass_cons<SAH_DQ>(ra, rb, rk, T.ray, rp, 0.001f, T.te, er) || right < 0;
-                if (left < 0) el = -F32_INF;
-                if (right < 0) er = -F32_INF;
+                if (STATS) st.c[ST_NODES]++;
+                const float4 nb = nodes_b[right];
+                pr = node_pass_cons<SAH_DQ>(nodes_a[right], nb, nkm[right], T.ray, rp, 0.001f, T.te, er);
+                rc = pack2(nb);
             }
             if (pl && pr) {
                 const bool lf = el <= er;
@@ -1761,9 +1686,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             } else {
                 pop();
             }
-        } else
-#endif
-        if (T.phase == ACT && T.node >= 0) {
+        } else if (T.phase == ACT && T.node >= 0) {
             if (STATS) st.c[ST_NODES]++;
             const float4 na = nodes_a[T.node];
             const float4 nb = nodes_b[T.node];
@@ -1820,12 +1743,6 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
 // decides as for any hit; a lane holding two tied leaves keeps the flag (re-traced on the reference
 // tree).  Rays of `todo` only (SAH rays: RTW_TF_SAH).  `audit` (tests only, RTW_COOP_AUDIT=1) takes
 // the DFS-last tied leaf instead: wrong images, which shows that the resolution decides them.
-#ifndef RTW_COOP_PIPE
-#define RTW_COOP_PIPE 1
-#endif
-#ifndef RTW_COOP_TE
-#define RTW_COOP_TE 1
-#endif
 template <int LDS, int LK>
 __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, unsigned long long todo, int32_t n_nodes,
                                         int32_t n_leaves, int32_t n_rects, int32_t fast_off, bool audit) {
@@ -1906,7 +1823,7 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
     // stops at t for most leaves and reads its record's second half only for closer ones (the drain's
     // waves read every record of every leaf per ray: LDS-bound)
     auto te_of = [](const CRay& c) {
-        return RTW_COOP_TE && c.best < F32_INF ? __int_as_float(__float_as_int(c.best) + 1) : F32_INF;
+        return c.best < F32_INF ? __int_as_float(__float_as_int(c.best) + 1) : F32_INF;
     };
     // (two rays per pass over the leaves, sharing the record reads, lost 2.4 % on suzanne and 3.7 % on
     // cornell_cube to spills: profiles/r04/v10_coop_ab.txt)
@@ -1917,16 +1834,10 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
         // software-pipelined: the next leaf record is read before this leaf's test, so that its LDS
         // latency overlaps the triangle / rect record read that depends on this one (one round trip per
         // leaf instead of two; the drain's rays are latency-bound)
-#if RTW_COOP_PIPE
         float4 sph_n = lane < n_leaves ? fast[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#endif
         for (int32_t leaf = lane; leaf < n_leaves; leaf += 64) {
-#if RTW_COOP_PIPE
             const float4 sph = sph_n;
             if (leaf + 64 < n_leaves) sph_n = fast[leaf + 64];
-#else
-            const float4 sph = fast[leaf];
-#endif
             float t;
             const float te = te_of(a);
             if (LK == LK_SPHERES || sph.w == sph.w) {
@@ -1938,7 +1849,7 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
                 keep(a, rect_t_mk(g, a.r, a.inv, 0.001f, te, t), t, leaf);  // SAH rays are Markstein-exact
             } else {
                 const int ti = __float_as_int(sph.y);
-                keep(a, tri_test(LDS == 2 ? load_tri_soa(tri_fast, RTW_TRI_BY_LEAF ? leaf : ti) : load_tri(tri_fast, ti), a.r,
+                keep(a, tri_test(LDS == 2 ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), a.r,
                                  0.001f, te, t),
                      t, leaf);
             }
@@ -1973,17 +1884,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         for (int i = threadIdx.x; i < 2 * A.rect_count; i += RTW_BLOCK) rects[i] = w.rects[i];
         if (LDS == 2) {
             float4* tris = rects + 2 * A.rect_count;
-            if (RTW_TRI_BY_LEAF) {  // component k of plain-triangle leaf l at k * RTW_TRI_SOA + l
-                for (int l = threadIdx.x; l < A.leaf_count; l += RTW_BLOCK) {
-                    const float4 f = w.leaf_fast[l];
-                    if (f.w != f.w && __float_as_int(f.x) == 1) {
-                        const int ti = __float_as_int(f.y);
-                        for (int k = 0; k < 4; ++k) tris[k * RTW_TRI_SOA + l] = w.tri_fast[4 * ti + k];
-                    }
-                }
-            } else {
-                for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[(i & 3) * RTW_TRI_SOA + (i >> 2)] = w.tri_fast[i];
-            }
+            for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[(i & 3) * RTW_TRI_SOA + (i >> 2)] = w.tri_fast[i];
         }
         if (A.sh_li >= 0) {  // shading tables (launch_render decides whether they fit)
             int4* li = reinterpret_cast<int4*>(smem + A.sh_li);
@@ -2057,7 +1958,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     // This wave's reserve of work items [w_next, w_end), in the local index space of its queue wq,
     // taken from the queue's counter in batches (one global atomic per batch, not per refill round);
     // batches shrink toward the end of the launch so that the last items still spread over all
-    // waves.  (RTW_PREFETCH 1 fetches the next batch one refill ahead instead.)
+    // waves.
     uint64_t w_next = 0, w_end = 0;
     uint32_t wq = (blockIdx.x * (RTW_BLOCK / 64) + (threadIdx.x >> 6)) % RTW_QUEUES;
     uint32_t qfail = 0;           // consecutive queues found empty: RTW_QUEUES of them end the launch
@@ -2123,7 +2024,6 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         __hip_atomic_store(&A.tune->tb[j - 1], wall_clock64(), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
-                if (!empty && RTW_PREFETCH) prefetch(leader);  // the next batch, in flight while this one is used
             }
             const uint64_t left = min(need, w_end - w_next);  // the first `left` lanes get an item
             const uint64_t first = w_next;
@@ -2234,7 +2134,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             T.node = w.root;
             if (sah) {  // the SAH walk needs the exact fast division; other rays take the reference tree
                 if (rp.fast) {
-                    T.node = LK == LK_SPHERES && RTW_C2_PACKED && RTW_C2_INLINE ? w.sah_root_c2 : w.sah_root;
+                    T.node = LK == LK_SPHERES ? w.sah_root_c2 : w.sah_root;
                     T.fast |= RTW_TF_SAH;
                 } else {
                     T.phase = PH_REF;
@@ -2992,7 +2892,8 @@ SahTables build_sah_tables(const rtw_world* w) {
                 if (!coord_ok(nd.min[k2]) || !coord_ok(nd.max[k2])) ok = false;
         // the extra nodes must not push a mesh world out of LDS mode 2 (its triangle records in LDS;
         // launch_render's sizing with the plain tree's depth as a floor): else the plain tree
-        if (ok && (RTW_TRI_BY_LEAF ? L : w->triangle_count) <= RTW_TRI_SOA) {
+        // (RTW_SAH_IGNORE_LDS=1, tests and audits: keep the split tree whatever the LDS mode)
+        if (ok && w->triangle_count <= RTW_TRI_SOA) {
             int32_t proot = 0;
             int pdepth = 0;
             std::vector<rtw_bvh_node> plain;
@@ -3002,7 +2903,7 @@ SahTables build_sah_tables(const rtw_world* w) {
                            (size_t)std::max(depth, pdepth) * RTW_BLOCK * 2;
                 };
                 const size_t cap = RTW_LDS_SCENE_MAX;
-                if (mode2(plain.size(), pdepth) <= cap && mode2(split.size(), sdepth) > cap) ok = false;
+                if (mode2(plain.size(), pdepth) <= cap && mode2(split.size(), sdepth) > cap && !std::getenv("RTW_SAH_IGNORE_LDS")) ok = false;
             }
         }
         if (ok) {
@@ -3689,7 +3590,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
     A.fast_off = 2 * A.node_count;
     int mode = 0;
-    if (g->tri_count > 0 && (RTW_TRI_BY_LEAF ? g->leaf_count : g->tri_count) <= RTW_TRI_SOA && g->leaf_count < 32768 &&
+    if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 &&
         A.node_count < 32768 &&
         g->node_count < 32768 && scene_bytes + tri_bytes + stack16_bytes <= cap)
         mode = 2;
@@ -3751,8 +3652,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     A.tune_items = 0;
     if (A.tune && A.total > 0 && !A.tile_perm) {  // epochs are whole passes: chunk-major order only
         const uint64_t lanes = (uint64_t)blocks * RTW_BLOCK;
-        const uint64_t lx = env_size("RTW_TUNE_LANES_X", 2);  // epoch length: at least lx x the resident lanes
-        const uint64_t E = (uint64_t)A.total * ((lx * lanes + A.total - 1) / A.total);
+        const uint64_t E = (uint64_t)A.total * ((2 * lanes + A.total - 1) / A.total);  // >= 2x the resident lanes
         if (A.items_big >= (uint64_t)(RTW_TUNE_EPOCHS + 2) * E) {
             A.tune_items = E;
             HIP_TRY(hipMemsetAsync(A.tune->tb, 0xFF, sizeof(A.tune->tb), stream));
@@ -3901,8 +3801,10 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
     // In-frame tuning of the dynamic-fetch threshold (TuneState): until a world has chosen one,
     // each render launch with room for it explores candidates over pass-aligned epochs.  RTW_TRACE_MIN
     // fixes the threshold instead.
+    // A whole-pixel frame keeps its fixed threshold even once an earlier per-sample frame of the world
+    // has chosen one: its lanes run whole pixels, not the tuned epochs' single samples.
     A.tune = nullptr;
-    if (!stats && !std::getenv("RTW_TRACE_MIN")) A.tune = g->tune;
+    if (!stats && !A.whole_pixel && !std::getenv("RTW_TRACE_MIN")) A.tune = g->tune;
     // Work order.  A frame renders tiles in the order of the deep-path cost its slots showed in
     // earlier frames of the same partition shape, costliest first, each tile's samples together:
     // the frame then ends on cheap tiles instead of waiting for paths trapped inside a mesh that

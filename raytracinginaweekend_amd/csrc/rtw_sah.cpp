@@ -157,6 +157,7 @@ struct SplitBuilder {
     std::vector<rtw_bvh_node>* nodes;
     std::vector<float>* km;  // 2 per node: the maxima over the leaves below
     int max_depth = 0;
+    bool bad = false;  // a reference box came out empty or not finite: the caller takes the object-split tree
     struct Out {
         int32_t id;
         float lo[3], hi[3];
@@ -218,6 +219,16 @@ struct SplitBuilder {
             olo[k] = std::max(olo[k], std::max(lo[k], r.lo[k]));
             ohi[k] = std::min(ohi[k], std::min(hi[k], r.hi[k]));
         }
+        // the clip can lose the whole polygon to rounding (a triangle grazing the cut): an empty box
+        // would round out to NaN (INF - INF) and vanish from a node union.  Keep the reference's box
+        // cut by [lo, hi] instead (it holds the part of the triangle inside, whatever the rounding)
+        bool empty = false;
+        for (int k = 0; k < 3; ++k) empty = empty || !(olo[k] <= ohi[k]);
+        if (empty)
+            for (int k = 0; k < 3; ++k) {
+                olo[k] = std::max(r.lo[k], lo[k]);
+                ohi[k] = std::min(r.hi[k], hi[k]);
+            }
     }
 
     Out build(std::vector<Ref>& refs, int depth) {
@@ -227,6 +238,8 @@ struct SplitBuilder {
             Out o;
             o.id = -1 - refs[0].leaf;
             round_out(refs[0].lo, refs[0].hi, o.lo, o.hi);
+            for (int k = 0; k < 3; ++k)  // every reference box finite and non-empty, or no split tree
+                if (!(std::isfinite(o.lo[k]) && std::isfinite(o.hi[k]) && o.lo[k] <= o.hi[k])) bad = true;
             const float k = lkm[2 * (size_t)refs[0].leaf], m = lkm[2 * (size_t)refs[0].leaf + 1];
             o.k = k < 0.0f ? 0.0f : k;  // a leaf that never reports a hit constrains nothing
             o.m = k < 0.0f ? 0.0f : m;
@@ -425,7 +438,7 @@ int sah_build_split(const float* lo, const float* hi, const float* tri, const fl
     nodes.reserve((size_t)n + (size_t)B.extra);
     *root = B.build(refs, 0).id;
     *depth = B.max_depth;
-    return 0;
+    return B.bad ? -1 : 0;
 }
 
 int sah_build(const float* lo, const float* hi, int32_t n, std::vector<rtw_bvh_node>& nodes, int32_t* root,

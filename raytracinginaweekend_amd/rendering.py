@@ -94,6 +94,57 @@ def render(
     return out
 
 
+def render_devices(
+    image_size: Size2i,
+    thread_count: int,
+    samples_per_pixel: int,
+    max_depth: int,
+    world: World,
+    render_mode: RenderMode = RenderMode.Default,
+    *,
+    devices=(0,),
+    seed: int = DEFAULT_SEED,
+    tile: tuple[int, int] = (8, 8),
+) -> np.ndarray:
+    """`render` on several GPUs of one node from one call (rtw_render_devices): entry i of `devices`
+    renders the interleaved tiles t % len(devices) == i on its own host thread, the tile buffers meet on
+    devices[0] over xGMI.  A device may repeat.  Bit-identical to `render` for every device list."""
+    p = render_params(image_size, samples_per_pixel, max_depth, render_mode, seed, tile=tile, thread_count=thread_count)
+    p.part_count = 0
+    out = np.zeros((image_size.height * image_size.width, 3), np.float32)
+    devs = (C.c_int * len(devices))(*devices)
+    check(lib().rtw_render_devices(world.ptr(), C.byref(p), devs, len(devices), out.ctypes.data_as(C.POINTER(C.c_float))))
+    return out
+
+
+class MultiDeviceWorld:
+    """A World resident on several GPUs (rtw_multi_create): each frame is split over the device list and
+    assembled on devices[0] (rtw_multi_render, synchronous)."""
+
+    def __init__(self, world: World, devices):
+        self.world = world
+        self.devices = list(devices)
+        h = C.c_void_p()
+        devs = (C.c_int * len(self.devices))(*self.devices)
+        check(lib().rtw_multi_create(world.ptr(), devs, len(self.devices), C.byref(h)))
+        self._h = h
+
+    def render_into(self, params: N.RenderParams, d_image_ptr: int) -> None:
+        """One frame into the W*H*3 f32 device buffer at d_image_ptr (on devices[0])."""
+        check(lib().rtw_multi_render(self._h, C.byref(params), C.c_void_p(d_image_ptr)))
+
+    def release(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().rtw_multi_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
 class DeviceWorld:
     """A World resident in one GPU's HBM (rtw_world_upload), rendered into torch/HIP buffers."""
 
@@ -135,6 +186,9 @@ class DeviceWorld:
     def last_frame(self) -> dict:
         """The shape of the last frame: render launches, whole-pixel work items (no colour buffer),
         and the dynamic-fetch threshold it ran with (the tuned one once chosen, else the default)."""
+        if not hasattr(lib(), "rtw_world_last_frame"):
+            # an older experiment build loaded through RTW_LIBRARY (A/B runs): the tuned threshold only
+            return {"launches": None, "whole_pixel": None, "trace_min": self.tuned_trace_min()}
         n, wp, tm = C.c_int(), C.c_int(), C.c_int()
         check(lib().rtw_world_last_frame(self._h, C.byref(n), C.byref(wp), C.byref(tm)))
         return {"launches": n.value, "whole_pixel": bool(wp.value == 1), "trace_min": tm.value}

@@ -63,3 +63,27 @@ def test_partition_floats_host_side():
     from raytracinginaweekend_amd.distributed import tile_slots
 
     assert n.value == len(tile_slots(R.Size2i(20, 12), (8, 8), (1, 3))) * 3
+
+
+def test_render_devices_arguments():
+    """rtw_render_devices / rtw_multi_create reject bad device lists before touching a GPU, and without a
+    GPU they fail loudly (no CPU fallback)."""
+    world = R.demo_world("final_scene1")
+    p = R.render_params(R.Size2i(16, 8), 1, 5)
+    out = np.zeros((16 * 8, 3), np.float32)
+    optr = out.ctypes.data_as(C.POINTER(C.c_float))
+    devs = (C.c_int * 2)(0, 0)
+    assert N.lib().rtw_render_devices(world.ptr(), C.byref(p), None, 2, optr) == N.RTW_ERR_INVALID_ARGUMENT
+    assert N.lib().rtw_render_devices(world.ptr(), C.byref(p), devs, 0, optr) == N.RTW_ERR_INVALID_ARGUMENT
+    assert N.lib().rtw_render_devices(world.ptr(), C.byref(p), devs, 2, None) == N.RTW_ERR_INVALID_ARGUMENT
+    h = C.c_void_p()
+    assert N.lib().rtw_multi_create(None, devs, 2, C.byref(h)) == N.RTW_ERR_INVALID_ARGUMENT
+    assert N.lib().rtw_multi_render(None, C.byref(p), None) == N.RTW_ERR_INVALID_ARGUMENT
+    assert N.lib().rtw_multi_release(None) == N.RTW_OK
+    if not _has_gpu():
+        with pytest.raises(N.RtwError) as e:
+            R.render_devices(R.Size2i(16, 8), 1, 1, 5, world, devices=(0, 0))
+        assert e.value.code == N.RTW_ERR_NO_DEVICE
+    bad = (C.c_int * 1)(-1)
+    rc = N.lib().rtw_render_devices(world.ptr(), C.byref(p), bad, 1, optr)
+    assert rc in (N.RTW_ERR_INVALID_ARGUMENT, N.RTW_ERR_NO_DEVICE)

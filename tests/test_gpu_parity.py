@@ -451,3 +451,109 @@ def test_two_children_walk_ties_and_grazing_hits(monkeypatch):
     sah = R.render(big, 1, 4, 50, world, seed=47)
     monkeypatch.setenv("RTW_NO_SAH", "1")
     assert_bit_identical(sah, R.render(big, 1, 4, 50, world, seed=47), "sphere tie world, SAH vs reference tree")
+
+
+def test_whole_pixel_threshold_stays_fixed_after_tuning(worlds, monkeypatch):
+    """a whole-pixel frame runs at its fixed threshold (16) even after a per-sample frame of
+    the same world has tuned one on the device."""
+    import torch
+
+    world = worlds("final_scene1")
+    dw = R.DeviceWorld(world, 0)
+    big = R.render_params(R.Size2i(1920, 1080), 12, 50, seed=3)
+    out = torch.empty(1920 * 1080 * 3, dtype=torch.float32, device="cuda:0")
+    dw.render_into(big, out.data_ptr(), 0)  # per-sample items, long enough to host the tuning epochs
+    torch.cuda.synchronize()
+    assert dw.last_frame()["whole_pixel"] == 0
+    assert dw.tuned_trace_min() > 0, "the per-sample frame did not tune a threshold"
+    monkeypatch.setenv("RTW_WHOLE_PIXEL", "1")
+    size = R.Size2i(64, 36)
+    small = torch.empty(64 * 36 * 3, dtype=torch.float32, device="cuda:0")
+    p = R.render_params(size, 5, 50, seed=3)
+    dw.render_into(p, small.data_ptr(), 0)
+    torch.cuda.synchronize()
+    lf = dw.last_frame()
+    assert lf["whole_pixel"] == 1 and lf["trace_min"] == 16, lf
+    assert_bit_identical(small.cpu().numpy().reshape(-1, 3), O.render(world, p), "whole pixel after tuning")
+
+
+def _sah_nodes(world, budget, monkeypatch) -> tuple:
+    """(SAH nodes, leaves) of the tree build_sah_tables makes at a spatial-split budget (host only)."""
+    import ctypes as C
+
+    from raytracinginaweekend_amd import _native as N
+
+    monkeypatch.setenv("RTW_SAH_SPLIT_BUDGET", str(budget))
+    fn = N.lib().rtw_debug_sah_tree
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+    out = (C.c_double * 10)()
+    N.check(fn(C.cast(world.ptr(), C.c_void_p), out))
+    assert out[4] == 1.0
+    return int(out[0]), world.raw.leaf_count
+
+
+def _split_tie_world():
+    """Ties on a spatially split tree: long slivers crossing near a hub (the shape of the OBJ fan bug's
+    origin triangles, obj_loader.rs:227-264, whose overlapping boxes spatial splits cut), twice over with
+    different materials (every hit on them is a tie between two leaves the splits reference several
+    times), above a row of spheres."""
+    wb = R.WorldBuilder()
+    mats = [wb.material_lambert_solid((0.8, 0.2, 0.2)), wb.material_lambert_solid((0.2, 0.8, 0.2)),
+            wb.material_metal_solid((0.7, 0.7, 0.7), 0.1), wb.material_dielectric(1.5)]
+    g = wb.new_group()
+    g.add(wb.new_obj_sphere(100.0, mats[0]).translate((0.0, -100.0, 0.0)))
+    for k in range(5):
+        g.add(wb.new_obj_sphere(0.25, mats[k % 4]).translate((-1.0 + 0.5 * k, 0.25, 1.0)))
+    hub = np.array([0.0, 1.2, -0.8], np.float32)
+    n = np.array([0.0, 0.0, 1.0], np.float32)
+    tris = []
+    rs = np.random.default_rng(5)
+    for _ in range(40):  # spikes: the fan bug's (v0, ORIGIN, v2) slivers radiating from one point
+        d = rs.normal(size=3)
+        d /= np.linalg.norm(d)
+        p = np.cross(d, [0.3, 1.0, 0.2])
+        p /= np.linalg.norm(p)
+        tip = hub + 1.5 * d
+        a, b = tip - 0.12 * p, tip + 0.12 * p
+        base = hub - 1.2 * d  # crossing near the hub (spikes through one common point get no split)
+        tris.append(list(base) + list(a) + list(b) + list(n) * 3 + [0.0] * 6)
+    fan = np.array(tris, np.float32)
+    g.add(wb.new_mesh(fan, mats[1]))
+    g.add(wb.new_mesh(fan, mats[2]))
+    cam = R.Camera.build().vertical_fov(40.0, 9.0 / 16.0).position((0.3, 1.2, 5.0)).look_at((0, 1, 0), (0, 0.8, 0)).build()
+    return g.build().finish(wb, R.BackgroundColor.sky(), cam)
+
+
+def test_spatial_split_tree_ties_bit_exact(monkeypatch):
+    """ties on a tree whose spatial splits duplicate the fan's coincident slivers (budget 4 extra
+    references per leaf, far above the default): a leaf met twice must not clear the tie flag another leaf
+    set in between.  Bit-exact against the oracle and the reference tree."""
+    world = _split_tie_world()
+    nodes, leaves = _sah_nodes(world, 4, monkeypatch)
+    assert nodes > leaves - 1, f"no spatial split: {nodes} nodes for {leaves} leaves"
+    assert _kernel_tree(world).startswith("sah")
+    size = R.Size2i(96, 54)
+    gpu = R.render(size, 1, 8, 50, world, seed=31)
+    assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=31)), "tie world, split tree")
+    big = R.Size2i(480, 270)
+    sah = R.render(big, 1, 4, 50, world, seed=31)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert_bit_identical(sah, R.render(big, 1, 4, 50, world, seed=31), "tie world split tree vs reference tree")
+
+
+def test_suzanne_large_split_budget_bit_exact(worlds, monkeypatch):
+    """suzanne on a spatial-split tree far beyond the default budget (4 extra references per leaf; the LDS
+    mode-2 guard off, RTW_SAH_IGNORE_LDS): its shared mesh edges give exact ties between leaves referenced
+    several times.  Bit-exact against the oracle and the reference tree."""
+    world = worlds("suzanne")
+    monkeypatch.setenv("RTW_SAH_IGNORE_LDS", "1")
+    nodes, leaves = _sah_nodes(world, 4, monkeypatch)
+    assert nodes > leaves + leaves // 2, f"{nodes} nodes for {leaves} leaves"
+    size = R.Size2i(48, 36)
+    gpu = R.render(size, 1, 4, 50, world, seed=11)
+    assert_bit_identical(gpu, O.render(world, R.render_params(size, 4, 50, seed=11)), "suzanne, split budget 4")
+    big = R.Size2i(320, 180)
+    sah = R.render(big, 1, 8, 50, world, seed=29)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert_bit_identical(sah, R.render(big, 1, 8, 50, world, seed=29), "suzanne split budget 4 vs reference tree")

@@ -13,7 +13,7 @@ for c in "$@"; do
   [ "$v" = base ] && lib=$GRAFT_REPO_ROOT/raytracinginaweekend_amd/librtw.so
   for s in $scenes; do
     out=$(env RTW_LIBRARY=$lib $e timeout -k 10 120 python bench.py --scene $s $AB_ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-stats --no-pmc --no-first-frame --no-thread-count --no-configs 2>/dev/null | grep '^{' | python -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['config']['trace_min'], d['config'].get('kernel'))") || exit $?
-    echo "$r $v [$e] $s $out" | tee -a gpurun_out/ab_mix.log
+    echo "$r $v [$e] $s $out" | tee -a ${AB_LOG:-gpurun_out/ab_mix.log}
   done
 done
 done

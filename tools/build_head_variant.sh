@@ -7,4 +7,4 @@ git show ${2:-HEAD}:raytracinginaweekend_amd/csrc/rtw_device.hip > ab_tmp.hip
   -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-atomics -fno-slp-vectorize $RTW_VARIANT_FLAGS -c -x hip ab_tmp.hip -o build/ab_tmp.o
 rm -f ab_tmp.hip
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../librtw_$1.so build/ab_tmp.o build/scene_builder.o \
-  build/demo_worlds.o build/rtw_common.o build/rtw_sort.o build/rtw_sah.o
+  build/demo_worlds.o build/rtw_common.o build/rtw_sort.o build/rtw_sah.o build/rtw_multi.o
