@@ -155,13 +155,18 @@ RTW_HD uint64_t rtw_splitmix64_next(uint64_t* x) {
 }
 
 /* "ctr" mode: one stream per (pixel, sample).  pixel = y*W + x of the full image, sample in
- * [0, spp).  The image is therefore independent of lane/thread/GPU assignment. */
+ * [0, spp).  The image is therefore independent of lane/thread/GPU assignment.
+ * The xoroshiro state is s0 = x = splitmix64's finalizer of (pixel, sample) ^ key, s1 a second,
+ * bijective xorshift-multiply round of x (the finalizer's avalanche makes streams of neighbouring
+ * pixels and samples independent).  Round 5: one finalizer per sample instead of three (their 64-bit
+ * multiplies were most of the kernel's per-sample stream setup); the ctr-vs-ref statistical check
+ * (tests/test_ref_mode.py) pins the streams' quality. */
 RTW_HD uint64_t rtw_seed_key(uint64_t seed) { return rtw_mix64(seed ^ 0x5EED5EED5EED5EEDull); }
 RTW_HD rtw_xoro rtw_sample_stream(uint64_t seed_key, uint32_t pixel, uint32_t sample) {
-    uint64_t x = rtw_mix64((((uint64_t)pixel) << 32 | (uint64_t)sample) ^ seed_key);
+    const uint64_t x = rtw_mix64((((uint64_t)pixel) << 32 | (uint64_t)sample) ^ seed_key);
     rtw_xoro r;
-    r.s0 = rtw_splitmix64_next(&x);
-    r.s1 = rtw_splitmix64_next(&x);
+    r.s0 = x;
+    r.s1 = (x ^ (x >> 32)) * 0xD6E8FEB86659FD93ull;
     if ((r.s0 | r.s1) == 0) r.s0 = 1;
     return r;
 }

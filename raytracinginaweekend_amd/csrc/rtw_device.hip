@@ -112,16 +112,17 @@ struct DWorld {
     // the kernel's own search tree (rtw_sah.cpp; node format of node_a / node_b) and each leaf's
     // proof box, its parent node's box in the reference tree (2 per leaf: {min.xyz, max.x},
     // {max.y, max.z, 0, 0}), for the verification (§5.5)
+    // the SAH tree's node_b is {max.y, max.z, bits(children), bits(cull constants)}: sah_kids and sah_km
+    // below (the constants live in the node record, one LDS read less per node step than a km array)
     const float4* sah_a;
     const float4* sah_b;
-    const float2* sah_km;
     const float4* leaf_box;
     // each leaf's place in the reference tree's DFS (coop_trace's tie resolution): {side bits, and
     // per axis the bits of the ancestors splitting on it}, bit 31 - k for the ancestor at depth k;
     // null when the reference tree is deeper than 32
     const uint4* leaf_key;
     int32_t sah_root;
-    int32_t sah_root_c2;  // the SAH root's children packed 16 + 16 bits (the two-children walk's lane state)
+    int32_t sah_root_c2;  // the SAH root's packed children word (the two-children walk's lane state)
     int32_t root;
     int32_t has_light;
 };
@@ -347,6 +348,15 @@ __device__ __forceinline__ float div_c(float a, float c, float yc) {
     r = a == 0.0f ? q : r;
     if (__builtin_expect(!(a == 0.0f || mk_a_ok(a)), 0)) r = a / c;
     return r;
+}
+// An image texel's channel, byte / 255.0 (texture.rs:30-31, `rgb8 as f32 / 255.0`): Markstein's
+// correction with RN(1/255) is exact for every dividend 1..255 (inside the guards), and 0 gives q = 0
+// exactly with r = 0: no guard and no branch (rtw_device_check_division test 6: all 256 bytes).
+// Three operations instead of the IEEE division's eleven, three times per texel.
+__device__ __forceinline__ float tex255(uint32_t byte) {
+    const float a = (float)byte, y = 1.0f / 255.0f;
+    const float q = a * y;
+    return __builtin_fmaf(__builtin_fmaf(-255.0f, q, a), y, q);
 }
 __device__ __forceinline__ float comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 __device__ __forceinline__ void setc(V3& a, int i, float v) {
@@ -1103,6 +1113,23 @@ __device__ __forceinline__ bool box_hit_cond_fast(float4 na, float4 nb, const Ra
     return dmin > 0.0f;
 }
 
+// The SAH tree's node record (build_sah_tables): node_b.z = axis | (left & 0x7FFF) << 2 | right << 17,
+// children as in rtw_bvh_node (>= 0 node, < 0 leaf -1 - index; 15-bit signed: worlds of < 2^14 nodes and
+// leaves); node_b.w = the cull constants k (high half) and m (low half) as bf16 rounded up -- at most
+// 2^-7 larger than the x17/16-widened f32 constants, so the node test stays conservative.
+__device__ __forceinline__ int32_t sah_left(int32_t bits) { return __builtin_amdgcn_sbfe(bits, 2u, 15u); }
+__device__ __forceinline__ int32_t sah_right(int32_t bits) { return bits >> 17; }
+__device__ __forceinline__ float2 sah_km(float4 nb) {
+    const uint32_t b = __float_as_uint(nb.w);
+    return make_float2(__uint_as_float(b & 0xFFFF0000u), __uint_as_float(b << 16));
+}
+inline uint32_t bf16_up(float x) {  // x >= 0 (or +inf): the smallest bf16 >= x, as its 16 bits
+    uint32_t b;
+    std::memcpy(&b, &x, 4);
+    if (b & 0xFFFFu) b = (b + 0x10000u) & 0xFFFF0000u;
+    return b >> 16;
+}
+
 // ---------------------------------------------------------------------------------------------
 // textures / materials / light / background
 // ---------------------------------------------------------------------------------------------
@@ -1169,8 +1196,7 @@ __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit
             pv = min(pv, (uint32_t)(im.z - 1));
             if (STATS) st.c[ST_TEXEL]++;
             const uint32_t px = w.texels[(size_t)im.x + (size_t)pv * (size_t)im.y + pu];
-            return v3((float)(px & 255u) / 255.0f, (float)((px >> 8) & 255u) / 255.0f,
-                      (float)((px >> 16) & 255u) / 255.0f);
+            return v3(tex255(px & 255u), tex255((px >> 8) & 255u), tex255((px >> 16) & 255u));
         }
         const int pi = t2.x;
         const float k = marble_k(w.perlin_ranvec + 768 * pi, w.perlin_perm + 768 * pi, w.perlin_bits[pi], h.pos.x,
@@ -1482,7 +1508,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     const DWorld& w = *wp;
     // the plain-triangle records' base, loaded once per call into scalar registers (the world
     // struct is read through a pointer; left in the loop it becomes a dependent global load)
-    const int32_t rect_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
+    // LDS: the SAH tree has no cull-constant section (they are in node_b.w)
+    const int32_t rect_off = 2 * n_nodes + n_leaves + (TM == TM_SAH ? 0 : (n_nodes + 1) / 2);
     const int32_t tri_off = rect_off + 2 * n_rects;
     const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
     const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
@@ -1494,7 +1521,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     const float4* nodes_a = LDS_SCENE ? smem : TM == TM_SAH ? w.sah_a : w.node_a;
     const float4* nodes_b = LDS_SCENE ? smem + off_b : TM == TM_SAH ? w.sah_b : w.node_b;
     const float4* fast = LDS_SCENE ? smem + off_f : w.leaf_fast;
-    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem) + off_k : TM == TM_SAH ? w.sah_km : w.node_km;
+    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem) + off_k : w.node_km;  // not TM_SAH
     // 16-bit entries in LDS mode 2 (its triangle records cap the world far below 2^15 nodes and
     // leaves): half the stack bytes, so that a deeper SAH tree still leaves room for the records
     using StackEntry = std::conditional_t<LDS == 2, int16_t, int32_t>;
@@ -1533,9 +1560,6 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // step (+0.9 %, profiles/r04/v4_experiments_ab.txt; worlds of < 2^15 nodes and leaves, checked at
     // upload).
     constexpr bool C2 = TM == TM_SAH && LK == LK_SPHERES;
-    auto pack2 = [](float4 nb) {  // {.., .., bits(left << 2 | axis), bits(right)} -> left | right << 16
-        return (int32_t)(((uint32_t)(__float_as_int(nb.z) >> 2) & 0xFFFFu) | ((uint32_t)__float_as_int(nb.w) << 16));
-    };
     // the SAH node test's k term: D^2 (two operations; every world gained 0.5 % over round 2's Dq form,
     // profiles/r03/v6_delta_d2_ab.txt)
     constexpr bool SAH_DQ = false;
@@ -1651,8 +1675,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             // (leaf children need no box: their own test follows); accepted children are visited
             // near first (a leaf first), the other one pushed.  Any visit order finds the same
             // closest root (§5.5 step 1), so only the work changes.
-            const int32_t left = (int32_t)(int16_t)(T.node & 0xFFFF);
-            const int32_t right = T.node >> 16;
+            const int32_t left = sah_left(T.node);
+            const int32_t right = sah_right(T.node);
             float el = F32_INF, er = F32_INF;
             bool pl = false, pr = false;
             int32_t lc = left, rc = right;  // what stands for an accepted child: its packed children
@@ -1664,8 +1688,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             } else {
                 if (STATS) st.c[ST_NODES]++;
                 const float4 nb = nodes_b[left];
-                pl = node_pass_cons<SAH_DQ>(nodes_a[left], nb, nkm[left], T.ray, rp, 0.001f, T.te, el);
-                lc = pack2(nb);
+                pl = node_pass_cons<SAH_DQ>(nodes_a[left], nb, sah_km(nb), T.ray, rp, 0.001f, T.te, el);
+                lc = __float_as_int(nb.z);
             }
             if (right < 0) {
                 if (STATS) st.c[ST_T_SPHERE]++;
@@ -1674,8 +1698,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             } else {
                 if (STATS) st.c[ST_NODES]++;
                 const float4 nb = nodes_b[right];
-                pr = node_pass_cons<SAH_DQ>(nodes_a[right], nb, nkm[right], T.ray, rp, 0.001f, T.te, er);
-                rc = pack2(nb);
+                pr = node_pass_cons<SAH_DQ>(nodes_a[right], nb, sah_km(nb), T.ray, rp, 0.001f, T.te, er);
+                rc = __float_as_int(nb.z);
             }
             if (pl && pr) {
                 const bool lf = el <= er;
@@ -1690,15 +1714,15 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             if (STATS) st.c[ST_NODES]++;
             const float4 na = nodes_a[T.node];
             const float4 nb = nodes_b[T.node];
-            const float2 km = nkm[T.node];
+            const float2 km = TM == TM_SAH ? sah_km(nb) : nkm[T.node];
             float entry;
             if (TM == TM_SAH ? node_pass_cons<SAH_DQ>(na, nb, km, T.ray, rp, 0.001f, T.te, entry)
                              : node_pass<FAST_ONLY>(na, nb, km, T.ray, rp, 0.001f, T.te)) {
                 if (STATS) db[DB_PASS_LANES]++;
                 const int32_t lbits = __float_as_int(nb.z);
-                const int32_t left = lbits >> 2;
+                const int32_t left = TM == TM_SAH ? sah_left(lbits) : lbits >> 2;
                 const int axis = lbits & 3;
-                const int32_t right = __float_as_int(nb.w);
+                const int32_t right = TM == TM_SAH ? sah_right(lbits) : __float_as_int(nb.w);
                 bool fwd = __builtin_amdgcn_ubfe((uint32_t)T.fast, (uint32_t)axis, 1u) != 0u;  // ray.d[axis] > 0
                 // SAH walk: a leaf child first (its hit shrinks te before the sibling subtree; suzanne
                 // +2.2 %, profiles/r02/v9_two_child_ab.txt)
@@ -1748,7 +1772,7 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
                                         int32_t n_leaves, int32_t n_rects, int32_t fast_off, bool audit) {
     const DWorld& w = *wp;
     constexpr bool LDS_SCENE = LDS >= 1;
-    const int32_t rect_off = 2 * n_nodes + n_leaves + (n_nodes + 1) / 2;
+    const int32_t rect_off = 2 * n_nodes + n_leaves;  // the SAH tree's LDS scene: no cull-constant section
     const int32_t tri_off = rect_off + 2 * n_rects;
     const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
     const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
@@ -1872,15 +1896,17 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     if (LDS_SCENE) {
         const float4* ga = sah ? w.sah_a : w.node_a;
         const float4* gb = sah ? w.sah_b : w.node_b;
-        const float2* gk = sah ? w.sah_km : w.node_km;
         for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) {
             smem[i] = ga[i];
             smem[A.node_count + i] = gb[i];
         }
         for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
+        // the reference tree's cull constants (the SAH tree keeps them in its node records)
+        const int32_t km_f4 = sah ? 0 : (A.node_count + 1) / 2;
         float2* km = reinterpret_cast<float2*>(smem + 2 * A.node_count + A.leaf_count);
-        for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = gk[i];
-        float4* rects = smem + 2 * A.node_count + A.leaf_count + (A.node_count + 1) / 2;
+        if (!sah)
+            for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = w.node_km[i];
+        float4* rects = smem + 2 * A.node_count + A.leaf_count + km_f4;
         for (int i = threadIdx.x; i < 2 * A.rect_count; i += RTW_BLOCK) rects[i] = w.rects[i];
         if (LDS == 2) {
             float4* tris = rects + 2 * A.rect_count;
@@ -2632,6 +2658,10 @@ __global__ void check_division_kernel(int test, uint64_t base, uint64_t n, uint6
             const uint64_t r1 = chk_mix(seed ^ (2 * i)), r2 = chk_mix(seed ^ (2 * i + 1));
             const float a = chk_float(r1, -80, 80), b = chk_float(r2, -22, 22);
             ok = chk_same(mk_corr(a, b, rcp_nr(b)), a / b);
+        } else if (test == 6) {
+            // tex255 (an image texel's channel) against byte / 255.0f: bytes base + i, i < 256
+            const uint32_t b = (uint32_t)(base + i) & 255u;
+            ok = chk_same(tex255(b), (float)b / 255.0f);
         } else if (test == 5) {
             // tri_t_mk: a dividend of any kind (zeros, subnormals, NaN, up to 2^40 in magnitude: num is a
             // dot product of coordinates below 2^30 with a unit normal), a divisor
@@ -2935,23 +2965,22 @@ SahTables build_sah_tables(const rtw_world* w) {
     if (const char* ll = std::getenv("RTW_SAH_LEAF_LEFT"); !(ll && ll[0] == '0'))
         for (rtw_bvh_node& n : nodes)
             if (n.left >= 0 && n.right < 0) std::swap(n.left, n.right);
+    // node records (sah_left / sah_right / sah_km): children 15-bit signed, so at most 2^14 - 1 nodes and
+    // 2^14 leaves (larger worlds walk the reference tree); the cull constants as bf16 rounded up
+    if (nodes.size() >= 16384 || L > 16384) return S;
+    auto kids = [](const rtw_bvh_node& n) {
+        return (int32_t)((uint32_t)n.axis | (((uint32_t)n.left & 0x7FFFu) << 2) | ((uint32_t)n.right << 17));
+    };
     S.a.resize(nodes.size());
     S.b.resize(nodes.size());
     for (size_t i = 0; i < nodes.size(); ++i) {
         const rtw_bvh_node& n = nodes[i];
+        const uint32_t kmb = (bf16_up(S.km[2 * i]) << 16) | bf16_up(S.km[2 * i + 1]);
         S.a[i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
-        S.b[i] = make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis), ibits(n.right));
+        S.b[i] = make_float4(n.max[1], n.max[2], ibits(kids(n)), ibits((int32_t)kmb));
     }
-    // plain-sphere worlds walk two children per step with the children packed 16 + 16 bits in the lane
-    // state and on the stack (traverse, C2P): their node and leaf indices must fit 16 bits
-    {
-        bool plain_spheres = true;
-        for (int32_t i = 0; i < L; ++i)
-            if (w->leaves[i].geom_kind != RTW_GEOM_SPHERE || w->leaves[i].flags != 0) plain_spheres = false;
-        if (plain_spheres && (nodes.size() >= 32767 || L >= 32767)) return S;
-        const rtw_bvh_node& r = nodes[(size_t)S.root];
-        S.root_c2 = (int32_t)(((uint32_t)r.left & 0xFFFFu) | ((uint32_t)r.right << 16));
-    }
+    // plain-sphere worlds walk two children per step with the root's children word as the first lane state
+    S.root_c2 = kids(nodes[(size_t)S.root]);
     S.box.resize((size_t)L * 2);
     for (int32_t i = 0; i < L; ++i) {
         const rtw_bvh_node& p = w->nodes[parent[(size_t)i]];
@@ -3224,7 +3253,6 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     const SahTables sah = build_sah_tables(w);
     const size_t o_sa = sah.ok ? L.push(sah.a.data(), sah.a.size() * sizeof(float4)) : 0;
     const size_t o_sb = sah.ok ? L.push(sah.b.data(), sah.b.size() * sizeof(float4)) : 0;
-    const size_t o_sk = sah.ok ? L.push(sah.km.data(), sah.km.size() * sizeof(float)) : 0;
     const size_t o_lb = sah.ok ? L.push(sah.box.data(), sah.box.size() * sizeof(float4)) : 0;
     const size_t o_lk = sah.ok && !sah.key.empty() ? L.push(sah.key.data(), sah.key.size() * sizeof(uint4)) : 0;
 
@@ -3275,7 +3303,6 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     if (sah.ok) {
         d.sah_a = (const float4*)(base + o_sa);
         d.sah_b = (const float4*)(base + o_sb);
-        d.sah_km = (const float2*)(base + o_sk);
         d.leaf_box = (const float4*)(base + o_lb);
         d.leaf_key = o_lk ? (const uint4*)(base + o_lk) : nullptr;
         d.sah_root = sah.root;
@@ -3365,7 +3392,8 @@ extern "C" RTW_API int rtw_debug_sah_tree(const rtw_world* w, double* out) {
     // ground sphere would otherwise make every mesh node's area vanish against the root's)
     int32_t root = S.root;
     if (root >= 0) {
-        const int32_t l = (int32_t)fbits(S.b[(size_t)root].z) >> 2, r = (int32_t)fbits(S.b[(size_t)root].w);
+        const int32_t kb = (int32_t)fbits(S.b[(size_t)root].z);
+        const int32_t l = (int32_t)((uint32_t)kb << 15) >> 17, r = kb >> 17;
         if ((l < 0) != (r < 0)) root = l >= 0 ? l : r;
     }
     double nodes = 1.0, leaves = 0.0;  // the top node's test; a child is tested when its parent passes
@@ -3377,7 +3405,8 @@ extern "C" RTW_API int rtw_debug_sah_tree(const rtw_world* w, double* out) {
             todo.pop_back();
             const double an = area(S.a[(size_t)i], S.b[(size_t)i]) / ar;
             for (int c = 0; c < 2; ++c) {
-                const int32_t ch = c ? (int32_t)fbits(S.b[(size_t)i].w) : ((int32_t)fbits(S.b[(size_t)i].z) >> 2);
+                const int32_t kb = (int32_t)fbits(S.b[(size_t)i].z);
+                const int32_t ch = c ? kb >> 17 : (int32_t)((uint32_t)kb << 15) >> 17;
                 (ch < 0 ? leaves : nodes) += an;
                 if (ch >= 0) todo.push_back(ch);
             }
@@ -3392,7 +3421,10 @@ extern "C" RTW_API int rtw_debug_sah_tree(const rtw_world* w, double* out) {
     // first, until 4): steps, box tests, leaf tests, all per ray by the area measure
     if (root >= 0) {
         const double ar = area(S.a[(size_t)root], S.b[(size_t)root]);
-        auto kids = [&](int32_t i, int c) { return c ? (int32_t)fbits(S.b[(size_t)i].w) : ((int32_t)fbits(S.b[(size_t)i].z) >> 2); };
+        auto kids = [&](int32_t i, int c) {
+            const int32_t kb = (int32_t)fbits(S.b[(size_t)i].z);
+            return c ? kb >> 17 : (int32_t)((uint32_t)kb << 15) >> 17;
+        };
         double st2 = 0.0, bx2 = 0.0, st4 = 0.0, bx4 = 0.0, lf4 = 0.0;
         std::vector<int32_t> todo{root};
         while (!todo.empty()) {
@@ -3584,10 +3616,10 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const size_t stack16_bytes = stack_bytes / 2;  // mode 2: 16-bit entries
     const char* lds_mode_env = std::getenv("RTW_LDS_MODE");  // audits: cap the mode
     A.node_count = sah ? g->sah_nodes : g->node_count;
-    // LDS scene: [node_a n][node_b n][leaf records L][cull constants (n + 1) / 2][rects 2R] (+ the triangle
-    // records in mode 2)
+    // LDS scene: [node_a n][node_b n][leaf records L][cull constants (n + 1) / 2, reference tree only][rects
+    // 2R] (+ the triangle records in mode 2)
     const size_t scene_bytes =
-        (size_t)(2 * A.node_count + g->leaf_count + (A.node_count + 1) / 2 + 2 * g->rect_count) * sizeof(float4);
+        (size_t)(2 * A.node_count + g->leaf_count + (sah ? 0 : (A.node_count + 1) / 2) + 2 * g->rect_count) * sizeof(float4);
     A.fast_off = 2 * A.node_count;
     int mode = 0;
     if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 &&
@@ -4154,7 +4186,7 @@ extern "C" RTW_API int rtw_device_eval_node_pass(int device, const float* box, c
 
 extern "C" RTW_API int rtw_device_check_division(int device, int test, uint64_t base, uint64_t n, uint64_t seed,
                                                  uint64_t* mismatches, uint64_t* first) {
-    if (!mismatches || !first || test < 0 || test > 5) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
+    if (!mismatches || !first || test < 0 || test > 6) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "bad argument");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rtw::fail(RTW_ERR_NO_DEVICE, "no HIP device");
     HIP_TRY(hipSetDevice(device));

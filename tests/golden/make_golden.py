@@ -59,10 +59,8 @@ def mix64(z: int) -> int:
 def sample_stream(seed: int, pixel: int, sample: int) -> tuple[int, int]:
     key = mix64((seed ^ 0x5EED5EED5EED5EED) & M64)
     x = mix64(((pixel << 32) | sample) ^ key)
-    x = (x + 0x9E3779B97F4A7C15) & M64
-    s0 = mix64(x)
-    x = (x + 0x9E3779B97F4A7C15) & M64
-    s1 = mix64(x)
+    s0 = x
+    s1 = ((x ^ (x >> 32)) * 0xD6E8FEB86659FD93) & M64
     return (s0 or 1) if (s0 | s1) == 0 else s0, s1
 
 

@@ -64,3 +64,10 @@ def test_triangle_t_without_guard():
     division whenever the quotient reaches ts = 0.001, and below ts whenever IEEE's is."""
     bad, first = _check(5, 0, 1 << 31, seed=0x7E57)
     assert bad == 0, f"{bad} mismatches, first case {first}"
+
+
+def test_texel_channel_every_byte():
+    """tex255 (an image texel's channel, texture.rs:30-31 `as f32 / 255.0`) by Markstein's correction
+    without a guard: equal to the IEEE division for all 256 byte values."""
+    bad, first = _check(6, 0, 256)
+    assert bad == 0, f"{bad} mismatches, first byte {first}"

@@ -15,6 +15,7 @@ set -o pipefail
 O=gpurun_out/${TAG:-run}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 nb=0
+nf=0
 for step in "$@"; do
   kind=${step%%:*}; rest=${step#*:}; [ "$rest" = "$step" ] && rest=""
   echo "== $step ($(date +%T))" | tee -a $O/steps.log
@@ -24,10 +25,11 @@ for step in "$@"; do
       timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
         > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; } ;;
     files)
+      nf=$((nf + 1))
       f=${rest%%:*}; e=${rest#*:}; [ "$e" = "$rest" ] && e=""
       if [ -z "$e" ]; then K=(); else K=(-k "$e"); fi
       timeout -k 10 1100 python -u -m pytest ${f//,/ } -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
-        > $O/gpu_tests_files.log 2>&1 || { tail -30 $O/gpu_tests_files.log; exit 1; } ;;
+        > $O/gpu_tests_files_$nf.log 2>&1 || { tail -30 $O/gpu_tests_files_$nf.log; exit 1; } ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1 ;;
     bench)
