@@ -76,7 +76,7 @@
 #endif
 #define RTW_STACK 32    // per-lane traversal stack (LDS), >= the BVH depth (checked at upload)
 #ifndef RTW_SAH_SPLIT_BUDGET
-#define RTW_SAH_SPLIT_BUDGET 0.2  // spatial splits in the SAH tree of triangle worlds: extra references per leaf
+#define RTW_SAH_SPLIT_BUDGET 1.0  // spatial splits in the SAH tree of triangle worlds: extra references per leaf
 #endif
 #ifndef RTW_LDS_SCENE_MAX
 #define RTW_COOP_MAX 32      // drain: live lanes at most for the wave-cooperative trace (RTW_COOP_MAX=0: off); 4: suzanne -1.1 %, its 8-way shares up to 64.5 ms against 59.4 (profiles/r04/v3_experiments_ab.txt, v4_...)
@@ -112,10 +112,12 @@ struct DWorld {
     // the kernel's own search tree (rtw_sah.cpp; node format of node_a / node_b) and each leaf's
     // proof box, its parent node's box in the reference tree (2 per leaf: {min.xyz, max.x},
     // {max.y, max.z, 0, 0}), for the verification (§5.5)
-    // the SAH tree's node_b is {max.y, max.z, bits(children), bits(cull constants)}: sah_kids and sah_km
-    // below (the constants live in the node record, one LDS read less per node step than a km array)
+    // the SAH tree: node_b as the reference tree's, cull constants in sah_km -- except in plain-sphere
+    // worlds (the two-children walk), whose node_b is {max.y, max.z, bits(children), m} (sah_left /
+    // sah_right) with the cull constants {sah_k, m}: the world's k, the node's m, and no sah_km
     const float4* sah_a;
     const float4* sah_b;
+    const float2* sah_km;
     const float4* leaf_box;
     // each leaf's place in the reference tree's DFS (coop_trace's tie resolution): {side bits, and
     // per axis the bits of the ancestors splitting on it}, bit 31 - k for the ancestor at depth k;
@@ -125,6 +127,7 @@ struct DWorld {
     int32_t sah_root_c2;  // the SAH root's packed children word (the two-children walk's lane state)
     int32_t root;
     int32_t has_light;
+    float sah_k;  // plain-sphere worlds' SAH tree: the largest finite node k (nodes of infinite k carry m = inf)
 };
 
 // Rarely-read scalars live in HBM (scalar-cache loads at their use sites) instead of kernel
@@ -236,6 +239,12 @@ struct KArgs {
     // the refill's batch divisor (RTW_BATCH_SPREAD x waves) and the tuner's epoch / half-epoch:
     // 64-bit divisions there expanded to ~140 instructions each
     FastDiv fd_spread, fd_epoch, fd_half;
+    // (last: fields read only by some kernel variants; ahead of the others they shifted the argument
+    // layout into more SGPR spills)
+    // the generic leaf path's tables in LDS (float4 offsets, -1: HBM / L2; render_kernel's GEN): leaf_xf
+    // (3 per leaf), spheres, boxes (2 per box); and the rects of the LDS scene
+    int32_t sh_xf, sh_sph, sh_bx, sh_rect;
+    int32_t sphere_count, box_count;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -508,6 +517,40 @@ struct Stats {
     uint32_t c[ST_COUNT];
 };
 
+// Where shading and the generic leaf path read their records: LDS float4 offsets (-1: HBM / L2).
+// The chain leaf record -> material -> texture is a run of dependent loads per shaded ray, so the
+// tables sit in LDS whenever they fit (launch_render), and a plain sphere's geometry comes from
+// its leaf_fast copy (`fast`, also in LDS).  The generic leaf path (Transformation / Animation /
+// volume leaves, boxes) reads the leaf record, its transform or velocity and then the primitive: a
+// chain of three dependent loads per leaf test, from LDS too when they fit (round 5: earth_motion's
+// two moving spheres, C5, waited on those global loads).
+// Whether the generic tables (xf, sph, bx) and the rects are in LDS is a compile-time property of the
+// kernel variant (GEN: render_kernel's template parameter, RECT: the LDS scene of a world with rect
+// leaves): as runtime choices their loads became pointer selects and flat loads, and their offsets
+// occupied SGPRs across the bounce loop (suzanne -3 % from the spills).
+extern __shared__ __attribute__((aligned(16))) float4 smem[];
+template <bool GEN, bool RECT>
+struct ShadeTabsT {
+    int32_t li, mat, tex0, fast;
+    int32_t xf, sph, bx, rect;  // leaf_xf, spheres, boxes (GEN), rects (RECT)
+    static constexpr bool gen = GEN, rect_lds = RECT;
+};
+using ShadeTabs = ShadeTabsT<false, false>;  // the tables of the device self-test kernels
+__device__ __forceinline__ int4 lds_i4(int32_t i) { return reinterpret_cast<const int4*>(smem)[i]; }
+template <class TB>
+__device__ __forceinline__ float4 tab_gen(const TB& S, int32_t off, const float4* __restrict__ g, int i) {
+    (void)S;
+    if constexpr (TB::gen) return smem[off + i];
+    else return g[i];
+}
+template <class TB>
+__device__ __forceinline__ int4 leaf_info_of(const DWorld& w, const TB& S, int leaf) {
+    int4 v;
+    if (S.li >= 0) v = lds_i4(S.li + leaf);
+    else v = w.leaf_info[leaf];
+    return v;
+}
+
 // ---------------------------------------------------------------------------------------------
 // primitives: candidate tests return t only
 // ---------------------------------------------------------------------------------------------
@@ -541,8 +584,16 @@ struct RectG {
     int plane;
     float dist, r00, r01, r10, r11;
 };
-__device__ __forceinline__ RectG load_rect(const DWorld& w, int i) {
-    const float4 a = w.rects[2 * i], b = w.rects[2 * i + 1];
+template <class TB>
+__device__ __forceinline__ RectG load_rect(const DWorld& w, const TB& S, int i) {
+    float4 a, b;
+    if constexpr (TB::rect_lds) {
+        a = smem[S.rect + 2 * i];
+        b = smem[S.rect + 2 * i + 1];
+    } else {
+        a = w.rects[2 * i];
+        b = w.rects[2 * i + 1];
+    }
     return RectG{__float_as_int(b.y), a.x, a.y, a.z, a.w, b.x};
 }
 // rect_geometry.rs:33-46 (hit test part)
@@ -596,10 +647,12 @@ __device__ __forceinline__ bool box_line(float4 ba, float4 bb, const Ray& r, flo
     ft = far;
     return true;
 }
-__device__ __forceinline__ bool box_t(const DWorld& w, int i, const Ray& r, float ts, float te, float& t) {
+template <class TB>
+__device__ __forceinline__ bool box_t(const DWorld& w, const TB& S, int i, const Ray& r, float ts, float te,
+                                      float& t) {
     float nt, ft;
     int np, fp;
-    if (!box_line(w.boxes[2 * i], w.boxes[2 * i + 1], r, nt, np, ft, fp)) return false;
+    if (!box_line(tab_gen(S, S.bx, w.boxes, 2 * i), tab_gen(S, S.bx, w.boxes, 2 * i + 1), r, nt, np, ft, fp)) return false;
     if (contains(ts, te, nt)) {
         t = nt;
         return true;
@@ -711,16 +764,16 @@ __device__ __forceinline__ bool tri_test(const TriFast& T, const Ray& r, float t
     return w2 > 0.0f && w0 > 0.0f;
 }
 
-template <bool STATS>
-__device__ __forceinline__ bool geom_t(const DWorld& w, int kind, int idx, const Ray& r, float ts, float te, float& t,
-                                       Stats& st) {
+template <bool STATS, class TB>
+__device__ __forceinline__ bool geom_t(const DWorld& w, const TB& S, int kind, int idx, const Ray& r, float ts,
+                                       float te, float& t, Stats& st) {
     if (STATS) st.c[ST_T_SPHERE + kind]++;
-    if (kind == RTW_GEOM_SPHERE) return sphere_t(w.spheres[idx], r, ts, te, t);
+    if (kind == RTW_GEOM_SPHERE) return sphere_t(tab_gen(S, S.sph, w.spheres, idx), r, ts, te, t);
     if (kind == RTW_GEOM_RECT) {
         V3 pos;
-        return rect_t(load_rect(w, idx), r, ts, te, t, pos);
+        return rect_t(load_rect(w, S, idx), r, ts, te, t, pos);
     }
-    if (kind == RTW_GEOM_BOX) return box_t(w, idx, r, ts, te, t);
+    if (kind == RTW_GEOM_BOX) return box_t(w, S, idx, r, ts, te, t);
     return tri_test(load_tri(w.tri_fast, idx), r, ts, te, t);
 }
 
@@ -745,39 +798,43 @@ __device__ __forceinline__ Ray xf_reverse(const Xf& x, const Ray& r) {
     o.time = r.time;
     return o;
 }
-__device__ __forceinline__ Xf anim_xf(const DWorld& w, int leaf, float time) {
-    const float4 b = w.leaf_xf[3 * leaf + 1], c = w.leaf_xf[3 * leaf + 2];
+template <class TB>
+__device__ __forceinline__ Xf anim_xf(const DWorld& w, const TB& S, int leaf, float time) {
+    const float4 b = tab_gen(S, S.xf, w.leaf_xf, 3 * leaf + 1), c = tab_gen(S, S.xf, w.leaf_xf, 3 * leaf + 2);
     const V3 vt = mul(v3(b.z, b.w, c.x), time);
     return Xf{v3(0.0f + vt.x, 0.0f + vt.y, 0.0f + vt.z), 0.0f, 1.0f};
 }
-__device__ __forceinline__ Xf leaf_xform(const DWorld& w, int leaf) {
-    const float4 a = w.leaf_xf[3 * leaf], b = w.leaf_xf[3 * leaf + 1];
+template <class TB>
+__device__ __forceinline__ Xf leaf_xform(const DWorld& w, const TB& S, int leaf) {
+    const float4 a = tab_gen(S, S.xf, w.leaf_xf, 3 * leaf), b = tab_gen(S, S.xf, w.leaf_xf, 3 * leaf + 1);
     return Xf{v3(a.y, a.z, a.w), b.x, b.y};
 }
 // the ray as seen by the leaf's primitive
-__device__ __forceinline__ Ray leaf_local_ray(const DWorld& w, int leaf, uint32_t flags, const Ray& r) {
+template <class TB>
+__device__ __forceinline__ Ray leaf_local_ray(const DWorld& w, const TB& S, int leaf, uint32_t flags,
+                                              const Ray& r) {
     Ray rr = r;
-    if (flags & RTW_LEAF_ANIMATION) rr = xf_reverse(anim_xf(w, leaf, r.time), rr);
-    if (flags & RTW_LEAF_TRANSFORM) rr = xf_reverse(leaf_xform(w, leaf), rr);
+    if (flags & RTW_LEAF_ANIMATION) rr = xf_reverse(anim_xf(w, S, leaf, r.time), rr);
+    if (flags & RTW_LEAF_TRANSFORM) rr = xf_reverse(leaf_xform(w, S, leaf), rr);
     return rr;
 }
 
 // SceneElement::hit for one leaf (candidate test: t only).  Volumes draw one f32 here.
 // VOL: the world may hold volume leaves (the only leaves that draw from the path's RNG during the
 // traversal); without them the RNG state never changes inside the loop
-template <bool STATS, bool VOL = true>
-__device__ __forceinline__ bool leaf_t(const DWorld& w, int leaf, const Ray& r, float ts, float te, rtw_xoro& rng,
-                                       float& t, Stats& st) {
-    const int4 info = w.leaf_info[leaf];
+template <bool STATS, bool VOL, class TB>
+__device__ __forceinline__ bool leaf_t(const DWorld& w, const TB& S, int leaf, const Ray& r, float ts, float te,
+                                       rtw_xoro& rng, float& t, Stats& st) {
+    const int4 info = leaf_info_of(w, S, leaf);
     const uint32_t flags = (uint32_t)info.w;
-    const Ray rr = (flags & (RTW_LEAF_ANIMATION | RTW_LEAF_TRANSFORM)) ? leaf_local_ray(w, leaf, flags, r) : r;
+    const Ray rr = (flags & (RTW_LEAF_ANIMATION | RTW_LEAF_TRANSFORM)) ? leaf_local_ray(w, S, leaf, flags, r) : r;
     const bool volume = VOL && (flags & RTW_LEAF_VOLUME) != 0;
     // VolumeGeometry::hit (hittable.rs:309-331): boundary hit over (-inf, inf), then from t0+0.001
     float lo = volume ? -F32_INF : ts, hi = volume ? F32_INF : te;
     float t0 = 0.0f;
     for (int pass = 0;; ++pass) {
         float tt;
-        if (!geom_t<STATS>(w, info.x, info.y, rr, lo, hi, tt, st)) return false;
+        if (!geom_t<STATS>(w, S, info.x, info.y, rr, lo, hi, tt, st)) return false;
         if (!volume) {
             t = tt;
             return true;
@@ -790,7 +847,7 @@ __device__ __forceinline__ bool leaf_t(const DWorld& w, int leaf, const Ray& r, 
         const float sm = rtw_maxr(t0, ts);
         const float em = rtw_minr(tt, te);
         if (sm >= em) return false;
-        const float nid = w.leaf_xf[3 * leaf].x;
+        const float nid = tab_gen(S, S.xf, w.leaf_xf, 3 * leaf).x;
         const float tv = rtw_maxr(sm, 0.0f) + nid * d_logf(d_gen_f32(&rng));
         if (tv > em) return false;
         t = tv;
@@ -814,20 +871,12 @@ __device__ __forceinline__ void from_ray(Hit& h, const Ray& r, V3 pos, V3 sn, fl
     h.u = u;
     h.v = v;
 }
-// Where shading reads its per-leaf, material and texture records: LDS float4 offsets (-1: HBM / L2).
-// The chain leaf record -> material -> texture is a run of dependent loads per shaded ray, so the
-// tables sit in LDS whenever they fit (launch_render), and a plain sphere's geometry comes from
-// its leaf_fast copy (`fast`, also in LDS).
-extern __shared__ __attribute__((aligned(16))) float4 smem[];
-struct ShadeTabs {
-    int32_t li, mat, tex0, fast;
-};
-__device__ __forceinline__ int4 lds_i4(int32_t i) { return reinterpret_cast<const int4*>(smem)[i]; }
+template <class TB>
 __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray& r, float t, Hit& h,
-                                            const ShadeTabs& S) {
-    const int4 info = S.li >= 0 ? lds_i4(S.li + leaf) : w.leaf_info[leaf];
+                                            const TB& S) {
+    const int4 info = leaf_info_of(w, S, leaf);
     const uint32_t flags = (uint32_t)info.w;
-    const Ray rr = leaf_local_ray(w, leaf, flags, r);
+    const Ray rr = leaf_local_ray(w, S, leaf, flags, r);
     const int kind = info.x, idx = info.y;
     if (flags & RTW_LEAF_VOLUME) {  // hittable.rs:333-340
         h.pos = at(rr, t);
@@ -838,7 +887,7 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
     } else if (kind == RTW_GEOM_SPHERE) {  // sphere_geometry.rs:42-52
         // a plain sphere's leaf_fast record is {centre, radius} (the same floats as spheres[idx])
         const float4 s = (S.fast >= 0 && (flags & (RTW_LEAF_TRANSFORM | RTW_LEAF_ANIMATION)) == 0)
-                             ? smem[S.fast + leaf] : w.spheres[idx];
+                             ? smem[S.fast + leaf] : tab_gen(S, S.sph, w.spheres, idx);
         const V3 pos = at(rr, t);
         const V3 sn = divs_x(sub(pos, v3(s.x, s.y, s.z)), s.w);
         // uv (vec3.rs:241-249) only reaches the image through an image texture; a pure function
@@ -852,7 +901,7 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         }
         from_ray(h, rr, pos, sn, u, v);
     } else if (kind == RTW_GEOM_RECT) {  // rect_geometry.rs:37-55
-        const RectG g = load_rect(w, idx);
+        const RectG g = load_rect(w, S, idx);
         int p0, p1, n;
         rect_axes(g.plane, p0, p1, n);
         const V3 pos = add(rr.o, mul(rr.d, t));
@@ -862,7 +911,7 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         setc(sn, n, -1.0f);
         from_ray(h, rr, pos, sn, u, v);
     } else if (kind == RTW_GEOM_BOX) {  // aabb.rs:80-101
-        const float4 ba = w.boxes[2 * idx], bb = w.boxes[2 * idx + 1];
+        const float4 ba = tab_gen(S, S.bx, w.boxes, 2 * idx), bb = tab_gen(S, S.bx, w.boxes, 2 * idx + 1);
         float nt, ft;
         int np, fp;
         box_line(ba, bb, rr, nt, np, ft, fp);
@@ -891,12 +940,12 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
     }
     // apply_hit_interaction, innermost wrapper first (hittable.rs:279-283)
     if (flags & RTW_LEAF_TRANSFORM) {
-        const Xf x = leaf_xform(w, leaf);
+        const Xf x = leaf_xform(w, S, leaf);
         h.pos = add(rot_up(x.yc, x.ys, h.pos), x.off);
         h.n = rot_up(x.yc, x.ys, h.n);
     }
     if (flags & RTW_LEAF_ANIMATION) {
-        const Xf x = anim_xf(w, leaf, r.time);
+        const Xf x = anim_xf(w, S, leaf, r.time);
         h.pos = add(rot_up(x.yc, x.ys, h.pos), x.off);
         h.n = rot_up(x.yc, x.ys, h.n);
     }
@@ -1113,22 +1162,16 @@ __device__ __forceinline__ bool box_hit_cond_fast(float4 na, float4 nb, const Ra
     return dmin > 0.0f;
 }
 
-// The SAH tree's node record (build_sah_tables): node_b.z = axis | (left & 0x7FFF) << 2 | right << 17,
-// children as in rtw_bvh_node (>= 0 node, < 0 leaf -1 - index; 15-bit signed: worlds of < 2^14 nodes and
-// leaves); node_b.w = the cull constants k (high half) and m (low half) as bf16 rounded up -- at most
-// 2^-7 larger than the x17/16-widened f32 constants, so the node test stays conservative.
+// The two-children walk's node record (build_sah_tables, plain-sphere worlds): node_b.z = axis |
+// (left & 0x7FFF) << 2 | right << 17, children as in rtw_bvh_node (>= 0 node, < 0 leaf -1 - index; 15-bit
+// signed: worlds of < 2^14 nodes and leaves); node_b.w = the node's cull constant m.  Its k is the world's
+// (DWorld::sah_k, the largest finite node k: a larger k only grows delta, so the test stays conservative,
+// DESIGN 5.2); a node whose k is infinite (no cull below it) carries m = +inf instead, which passes it as
+// k = inf did.  The lane carries node_b.z itself as its packed children.  (The one-child walk of other
+// worlds keeps {left << 2 | axis, right} and a cull-constant array: the folded record ran suzanne 2.7 %
+// and cornell_cube 3 % slower, profiles/r05/ab_km.txt.)
 __device__ __forceinline__ int32_t sah_left(int32_t bits) { return __builtin_amdgcn_sbfe(bits, 2u, 15u); }
 __device__ __forceinline__ int32_t sah_right(int32_t bits) { return bits >> 17; }
-__device__ __forceinline__ float2 sah_km(float4 nb) {
-    const uint32_t b = __float_as_uint(nb.w);
-    return make_float2(__uint_as_float(b & 0xFFFF0000u), __uint_as_float(b << 16));
-}
-inline uint32_t bf16_up(float x) {  // x >= 0 (or +inf): the smallest bf16 >= x, as its 16 bits
-    uint32_t b;
-    std::memcpy(&b, &x, 4);
-    if (b & 0xFFFFu) b = (b + 0x10000u) & 0xFFFF0000u;
-    return b >> 16;
-}
 
 // ---------------------------------------------------------------------------------------------
 // textures / materials / light / background
@@ -1172,9 +1215,9 @@ __device__ __forceinline__ float marble_k(const float* ranvec, const uint32_t* p
 
 // TX: the world's textures are all SolidColor (TX_SOLID) or not (TX_ANY: checker, marble, image)
 enum { TX_SOLID = 0, TX_ANY = 1 };
-template <bool STATS, int TX>
+template <bool STATS, int TX, class TB>
 __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit& h, Stats& st,
-                                             const ShadeTabs& S) {  // texture.rs:23-53
+                                             const TB& S) {  // texture.rs:23-53
     for (int guard = 0; guard < 64; ++guard) {
         const int4 t0 = S.tex0 >= 0 ? lds_i4(S.tex0 + tex) : w.textures[3 * tex];
         const int kind = t0.x;
@@ -1307,9 +1350,9 @@ struct ShadeOut {
     uint32_t texels;
 };
 
-template <bool STATS, int TX>
+template <bool STATS, int TX, class TB>
 __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t mode, Path P, int32_t found, float te,
-                                       float pdot, const ShadeTabs& S) {
+                                       float pdot, const TB& S) {
     const DWorld& w = *wp;
     Stats st;
     st.c[ST_TEXEL] = 0;
@@ -1497,10 +1540,10 @@ struct Trav {
 // the RNG update alone made the compiler copy the lane's traversal registers at the leaf merge on
 // every leaf step.
 enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_WRAPPED = 3, LK_ANY = 4 };
-template <bool STATS, int LDS, int LK, bool FAST_ONLY, int TM = TM_REF>
-__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, int32_t trace_min, int32_t n_nodes,
-                                      int32_t n_leaves, int32_t n_rects, int32_t n_tris, int32_t stack_off,
-                                      unsigned long long* dbg, int32_t coop_exit = -1) {
+template <bool STATS, int LDS, int LK, bool FAST_ONLY, int TM, class TB>
+__device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB& S, Trav T, int32_t trace_min,
+                                      int32_t n_nodes, int32_t n_leaves, int32_t n_rects, int32_t n_tris,
+                                      int32_t stack_off, unsigned long long* dbg, int32_t coop_exit = -1) {
     // the LDS holds the tree this mode walks (the SAH tree in SAH mode); the fallback reads HBM
     constexpr bool LDS_SCENE = LDS >= 1 && TM != TM_FALLBACK;
     constexpr int ACT = TM == TM_FALLBACK ? PH_REF : PH_TRACE;  // the lanes this loop advances
@@ -1509,7 +1552,8 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // the plain-triangle records' base, loaded once per call into scalar registers (the world
     // struct is read through a pointer; left in the loop it becomes a dependent global load)
     // LDS: the SAH tree has no cull-constant section (they are in node_b.w)
-    const int32_t rect_off = 2 * n_nodes + n_leaves + (TM == TM_SAH ? 0 : (n_nodes + 1) / 2);
+    constexpr bool C2 = TM == TM_SAH && LK == LK_SPHERES;  // the two-children walk (below)
+    const int32_t rect_off = 2 * n_nodes + n_leaves + (C2 ? 0 : (n_nodes + 1) / 2);
     const int32_t tri_off = rect_off + 2 * n_rects;
     const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
     const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
@@ -1518,13 +1562,17 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // loop's exec masks and get spilled to VGPR lanes, costing a v_readlane per node step.
     int32_t off_b = n_nodes, off_f = 2 * n_nodes, off_k = 2 * (2 * n_nodes + n_leaves);
     if (LDS_SCENE) asm volatile("" : "+v"(off_b), "+v"(off_f), "+v"(off_k));
+    // the two-children walk's k, also in a VGPR (a scalar would join the spilled SGPRs)
+    float sah_k = C2 ? w.sah_k : 0.0f;
+    if (C2) asm volatile("" : "+v"(sah_k));
     const float4* nodes_a = LDS_SCENE ? smem : TM == TM_SAH ? w.sah_a : w.node_a;
     const float4* nodes_b = LDS_SCENE ? smem + off_b : TM == TM_SAH ? w.sah_b : w.node_b;
     const float4* fast = LDS_SCENE ? smem + off_f : w.leaf_fast;
-    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem) + off_k : w.node_km;  // not TM_SAH
-    // 16-bit entries in LDS mode 2 (its triangle records cap the world far below 2^15 nodes and
-    // leaves): half the stack bytes, so that a deeper SAH tree still leaves room for the records
-    using StackEntry = std::conditional_t<LDS == 2, int16_t, int32_t>;
+    const float2* nkm = LDS_SCENE ? reinterpret_cast<const float2*>(smem) + off_k : TM == TM_SAH ? w.sah_km : w.node_km;
+    // 16-bit entries in the LDS modes (launch_render takes them only for worlds of < 2^15 nodes and
+    // leaves): half the stack bytes, room for a deeper SAH tree or the triangle records -- except in
+    // plain-sphere worlds, whose two-children walk pushes packed children words
+    using StackEntry = std::conditional_t<(LDS == 2 || (LDS == 1 && LK != LK_SPHERES)), int16_t, int32_t>;
     StackEntry* stack = reinterpret_cast<StackEntry*>(smem + stack_off) + threadIdx.x;
     // a leaf's root t: the reference narrows te to it; the SAH walk keeps te = succ(closest t) so
     // that a leaf reporting exactly the closest t again (a tie, whose winner is the reference's
@@ -1559,7 +1607,6 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
     // step (nodes_b.zw), and a pushed node is pushed as its children -- one dependent LDS read less per
     // step (+0.9 %, profiles/r04/v4_experiments_ab.txt; worlds of < 2^15 nodes and leaves, checked at
     // upload).
-    constexpr bool C2 = TM == TM_SAH && LK == LK_SPHERES;
     // the SAH node test's k term: D^2 (two operations; every world gained 0.5 % over round 2's Dq form,
     // profiles/r03/v6_delta_d2_ab.txt)
     constexpr bool SAH_DQ = false;
@@ -1598,7 +1645,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
                 take(t, leaf);
         } else if (LK >= LK_WRAPPED) {
             float t;
-            if (leaf_t<STATS, LK == LK_ANY>(w, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) take(t, leaf);
+            if (leaf_t<STATS, LK == LK_ANY>(w, S, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) take(t, leaf);
         }
     };
 
@@ -1688,7 +1735,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             } else {
                 if (STATS) st.c[ST_NODES]++;
                 const float4 nb = nodes_b[left];
-                pl = node_pass_cons<SAH_DQ>(nodes_a[left], nb, sah_km(nb), T.ray, rp, 0.001f, T.te, el);
+                pl = node_pass_cons<SAH_DQ>(nodes_a[left], nb, make_float2(sah_k, nb.w), T.ray, rp, 0.001f, T.te, el);
                 lc = __float_as_int(nb.z);
             }
             if (right < 0) {
@@ -1698,7 +1745,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             } else {
                 if (STATS) st.c[ST_NODES]++;
                 const float4 nb = nodes_b[right];
-                pr = node_pass_cons<SAH_DQ>(nodes_a[right], nb, sah_km(nb), T.ray, rp, 0.001f, T.te, er);
+                pr = node_pass_cons<SAH_DQ>(nodes_a[right], nb, make_float2(sah_k, nb.w), T.ray, rp, 0.001f, T.te, er);
                 rc = __float_as_int(nb.z);
             }
             if (pl && pr) {
@@ -1714,15 +1761,15 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, Trav T, 
             if (STATS) st.c[ST_NODES]++;
             const float4 na = nodes_a[T.node];
             const float4 nb = nodes_b[T.node];
-            const float2 km = TM == TM_SAH ? sah_km(nb) : nkm[T.node];
+            const float2 km = nkm[T.node];
             float entry;
             if (TM == TM_SAH ? node_pass_cons<SAH_DQ>(na, nb, km, T.ray, rp, 0.001f, T.te, entry)
                              : node_pass<FAST_ONLY>(na, nb, km, T.ray, rp, 0.001f, T.te)) {
                 if (STATS) db[DB_PASS_LANES]++;
                 const int32_t lbits = __float_as_int(nb.z);
-                const int32_t left = TM == TM_SAH ? sah_left(lbits) : lbits >> 2;
+                const int32_t left = lbits >> 2;
                 const int axis = lbits & 3;
-                const int32_t right = TM == TM_SAH ? sah_right(lbits) : __float_as_int(nb.w);
+                const int32_t right = __float_as_int(nb.w);
                 bool fwd = __builtin_amdgcn_ubfe((uint32_t)T.fast, (uint32_t)axis, 1u) != 0u;  // ray.d[axis] > 0
                 // SAH walk: a leaf child first (its hit shrinks te before the sibling subtree; suzanne
                 // +2.2 %, profiles/r02/v9_two_child_ab.txt)
@@ -1772,7 +1819,8 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
                                         int32_t n_leaves, int32_t n_rects, int32_t fast_off, bool audit) {
     const DWorld& w = *wp;
     constexpr bool LDS_SCENE = LDS >= 1;
-    const int32_t rect_off = 2 * n_nodes + n_leaves;  // the SAH tree's LDS scene: no cull-constant section
+    // the SAH tree's LDS scene: plain-sphere worlds have no cull-constant section
+    const int32_t rect_off = 2 * n_nodes + n_leaves + (LK == LK_SPHERES ? 0 : (n_nodes + 1) / 2);
     const int32_t tri_off = rect_off + 2 * n_rects;
     const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
     const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
@@ -1883,7 +1931,7 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
     return T;
 }
 
-template <bool STATS, int LDS, int LK, int TX>
+template <bool STATS, int LDS, int LK, int TX, bool GEN>
 __device__ __forceinline__ void render_body(const KArgs& A) {
     constexpr bool LDS_SCENE = LDS >= 1;
     // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
@@ -1901,11 +1949,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             smem[A.node_count + i] = gb[i];
         }
         for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
-        // the reference tree's cull constants (the SAH tree keeps them in its node records)
-        const int32_t km_f4 = sah ? 0 : (A.node_count + 1) / 2;
+        // the cull constants (the plain-sphere worlds' SAH tree keeps them in its node records)
+        const bool km_rec = sah && LK == LK_SPHERES;
+        const int32_t km_f4 = km_rec ? 0 : (A.node_count + 1) / 2;
         float2* km = reinterpret_cast<float2*>(smem + 2 * A.node_count + A.leaf_count);
-        if (!sah)
-            for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = w.node_km[i];
+        const float2* gk = sah ? w.sah_km : w.node_km;
+        if (!km_rec)
+            for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = gk[i];
         float4* rects = smem + 2 * A.node_count + A.leaf_count + km_f4;
         for (int i = threadIdx.x; i < 2 * A.rect_count; i += RTW_BLOCK) rects[i] = w.rects[i];
         if (LDS == 2) {
@@ -1919,6 +1969,11 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             for (int i = threadIdx.x; i < A.material_count; i += RTW_BLOCK) mt[i] = w.materials[i];
             if (A.sh_box >= 0)
                 for (int i = threadIdx.x; i < 2 * A.leaf_count; i += RTW_BLOCK) smem[A.sh_box + i] = w.leaf_box[i];
+            if (A.sh_xf >= 0) {
+                for (int i = threadIdx.x; i < 3 * A.leaf_count; i += RTW_BLOCK) smem[A.sh_xf + i] = w.leaf_xf[i];
+                for (int i = threadIdx.x; i < A.sphere_count; i += RTW_BLOCK) smem[A.sh_sph + i] = w.spheres[i];
+                for (int i = threadIdx.x; i < 2 * A.box_count; i += RTW_BLOCK) smem[A.sh_bx + i] = w.boxes[i];
+            }
             if (A.sh_tex0 >= 0) {
                 int4* tx = reinterpret_cast<int4*>(smem + A.sh_tex0);
                 for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
@@ -1928,7 +1983,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     }
     // the traversal stacks follow the LDS scene and the shading tables
     const int32_t stack_off = LDS_SCENE ? A.stack_off : 0;
-    const ShadeTabs stabs{A.sh_li, A.sh_mat, A.sh_tex0, A.sh_li >= 0 ? A.fast_off : -1};
+    // the generic tables only where the world's leaf kinds can read them (compile-time -1 elsewhere: their
+    // offsets would otherwise occupy SGPRs across the bounce loop, which spills -- suzanne -3 %)
+    ShadeTabsT<GEN, LDS_SCENE && LK >= LK_PLAIN> stabs{A.sh_li, A.sh_mat, A.sh_tex0, A.sh_li >= 0 ? A.fast_off : -1,
+                                                       GEN ? A.sh_xf : -1, GEN ? A.sh_sph : -1, GEN ? A.sh_bx : -1,
+                                                       LDS_SCENE && LK >= LK_PLAIN ? A.sh_rect : -1};
+    // the shading tables' offsets in VGPRs: as SGPRs they are live across the bounce loop and spill
+    asm volatile("" : "+v"(stabs.li), "+v"(stabs.mat), "+v"(stabs.tex0), "+v"(stabs.fast));
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
@@ -2183,7 +2244,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 #ifdef RTW_WAVE_TIMING
             uint64_t wx_t0 = wall_clock64();
 #endif
-            T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
+            T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, stabs, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
                                                        A.leaf_count, A.rect_count, A.tri_count, stack_off,
                                                        STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
             // the rays coop_trace takes (one call site, inlined: as an out-of-line call taking and
@@ -2253,18 +2314,18 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             const uint64_t wx_t2 = wall_clock64();
 #endif
             if (__ballot(T.phase == PH_REF) != 0)
-                T = traverse<STATS, LDS, LK, false, TM_FALLBACK>(A.wdev, T, 0, A.node_count, A.leaf_count, A.rect_count,
+                T = traverse<STATS, LDS, LK, false, TM_FALLBACK>(A.wdev, stabs, T, 0, A.node_count, A.leaf_count, A.rect_count,
                                                                  A.tri_count, stack_off,
                                                                  STATS ? A.stats + ST_COUNT : nullptr);
 #ifdef RTW_WAVE_TIMING
             if (qfail >= RTW_QUEUES) wx_tref += wall_clock64() - wx_t2;
 #endif
         } else if (__ballot(T.phase == PH_TRACE && (T.fast & 8) == 0) == 0) {
-            T = traverse<STATS, LDS, LK, true>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
+            T = traverse<STATS, LDS, LK, true, TM_REF>(A.wdev, stabs, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
                                                A.leaf_count, A.rect_count, A.tri_count, stack_off,
                                                STATS ? A.stats + ST_COUNT : nullptr);
         } else {
-            T = traverse<STATS, LDS, LK, false>(A.wdev, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
+            T = traverse<STATS, LDS, LK, false, TM_REF>(A.wdev, stabs, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
                                                 A.leaf_count, A.rect_count, A.tri_count, stack_off,
                                                 STATS ? A.stats + ST_COUNT : nullptr);
         }
@@ -2379,12 +2440,12 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     }
 }
 
-template <bool STATS, int LDS, int LK, int TX>
+template <bool STATS, int LDS, int LK, int TX, bool GEN = false>
 __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
 #ifdef RTW_WAVE_TIMING
     const uint64_t t_start = wall_clock64();
 #endif
-    render_body<STATS, LDS, LK, TX>(A);
+    render_body<STATS, LDS, LK, TX, GEN>(A);
 #ifdef RTW_WAVE_TIMING
     const uint32_t wv = (blockIdx.x * RTW_BLOCK + threadIdx.x) / 64;
     if ((threadIdx.x & 63) == 0 && wv < 8192) {
@@ -2839,7 +2900,9 @@ struct SahTables {
     std::vector<float> km;        // cull constants, 2 per node
     std::vector<float4> box;      // 2 per leaf: the proof box (the leaf's parent box in the reference tree)
     std::vector<uint4> key;       // per leaf: its DFS key material (DWorld::leaf_key), empty if too deep
-    int32_t root_c2 = 0;  // the root's children, 16 + 16 bits (the two-children walk, plain-sphere worlds)
+    int32_t root_c2 = 0;  // the root's children word (the two-children walk, plain-sphere worlds)
+    float k = 0.0f;       // the largest finite node k (DWorld::sah_k)
+    bool folded = false;  // plain-sphere world: node records carry children word + m (sah_left / sah_right)
     int32_t root = 0, depth = 0;
     bool ok = false;
 };
@@ -2891,7 +2954,8 @@ SahTables build_sah_tables(const rtw_world* w) {
     std::vector<rtw_bvh_node> nodes;
     // spatial splits (rtw::sah_build_split) in worlds with plain triangles, RTW_SAH_SPLIT_BUDGET extra
     // references per leaf at most (0: the object-split tree)
-    // (default 0.2: suzanne +1.1 %, cornell_cube +0.1 %, profiles/r04/v2_experiments_ab.txt)
+    // (default 1.0: suzanne +21 % over round 4's 0.2, now that a 16-bit stack keeps the larger tree in LDS
+    // mode 1, profiles/r05/split_stats.txt; round 4 measured 0.2 at +1.1 % over none)
     double budget = RTW_SAH_SPLIT_BUDGET;
     if (const char* e = std::getenv("RTW_SAH_SPLIT_BUDGET")) budget = std::max(0.0, std::atof(e));
     std::vector<float> tri;
@@ -2920,20 +2984,27 @@ SahTables build_sah_tables(const rtw_world* w) {
         for (const rtw_bvh_node& nd : split)
             for (int k2 = 0; k2 < 3; ++k2)
                 if (!coord_ok(nd.min[k2]) || !coord_ok(nd.max[k2])) ok = false;
-        // the extra nodes must not push a mesh world out of LDS mode 2 (its triangle records in LDS;
-        // launch_render's sizing with the plain tree's depth as a floor): else the plain tree
-        // (RTW_SAH_IGNORE_LDS=1, tests and audits: keep the split tree whatever the LDS mode)
-        if (ok && w->triangle_count <= RTW_TRI_SOA) {
+        // The extra nodes must not push the world out of the LDS modes (launch_render: mode 1 holds
+        // nodes, leaf records, cull constants, rects and the 16-bit stack, mode 2 the triangle records
+        // too): a split tree that fits mode 1 only beats the object-split tree in mode 2 (suzanne at
+        // budget 1, 1809 nodes, depth 20: 22.9 node visits and 10.3 triangle tests per ray against 30.8
+        // and 16.2 at budget 0.2, 1080p x 128 in 101.7 ms against 123.5, profiles/r05/split_stats.txt),
+        // but one that leaves the LDS entirely does not (else the plain tree).  RTW_SAH_IGNORE_LDS=1
+        // (tests and audits) keeps the split tree whatever the LDS mode.
+        if (ok) {
             int32_t proot = 0;
             int pdepth = 0;
             std::vector<rtw_bvh_node> plain;
             if (rtw::sah_build(lo.data(), hi.data(), L, plain, &proot, &pdepth) == 0) {
-                auto mode2 = [&](size_t n, int depth) {
-                    return (2 * n + (size_t)L + (n + 1) / 2) * 16 + (size_t)4 * RTW_TRI_SOA * 16 +
-                           (size_t)std::max(depth, pdepth) * RTW_BLOCK * 2;
+                int rdepth = 0;  // the reference tree's depth: the stack serves both walks
+                check_world(w, &rdepth);
+                auto mode1 = [&](size_t n, int depth) {
+                    return (2 * n + (size_t)L + (n + 1) / 2 + 2 * (size_t)w->rect_count) * 16 +
+                           (size_t)std::max(depth, rdepth) * RTW_BLOCK * 2;
                 };
                 const size_t cap = RTW_LDS_SCENE_MAX;
-                if (mode2(plain.size(), pdepth) <= cap && mode2(split.size(), sdepth) > cap && !std::getenv("RTW_SAH_IGNORE_LDS")) ok = false;
+                if (mode1(plain.size(), pdepth) <= cap && mode1(split.size(), sdepth) > cap && !std::getenv("RTW_SAH_IGNORE_LDS"))
+                    ok = false;
             }
         }
         if (ok) {
@@ -2965,21 +3036,31 @@ SahTables build_sah_tables(const rtw_world* w) {
     if (const char* ll = std::getenv("RTW_SAH_LEAF_LEFT"); !(ll && ll[0] == '0'))
         for (rtw_bvh_node& n : nodes)
             if (n.left >= 0 && n.right < 0) std::swap(n.left, n.right);
-    // node records (sah_left / sah_right / sah_km): children 15-bit signed, so at most 2^14 - 1 nodes and
-    // 2^14 leaves (larger worlds walk the reference tree); the cull constants as bf16 rounded up
-    if (nodes.size() >= 16384 || L > 16384) return S;
+    // plain-sphere worlds (the two-children walk): node records sah_left / sah_right with m, children
+    // 15-bit signed (at most 2^14 - 1 nodes and 2^14 leaves, else the reference tree), k per world
+    // (DWorld::sah_k), the root's children word as the walk's first lane state; other worlds: node_b as
+    // the reference tree's and the cull constants in sah_km
+    bool plain_spheres = true;
+    for (int32_t i = 0; i < L; ++i)
+        if (w->leaves[i].geom_kind != RTW_GEOM_SPHERE || w->leaves[i].flags != 0) plain_spheres = false;
+    S.folded = plain_spheres;
+    if (plain_spheres && (nodes.size() >= 16384 || L > 16384)) return S;
     auto kids = [](const rtw_bvh_node& n) {
         return (int32_t)((uint32_t)n.axis | (((uint32_t)n.left & 0x7FFFu) << 2) | ((uint32_t)n.right << 17));
     };
+    S.k = 0.0f;
+    for (size_t i = 0; i < nodes.size(); ++i)
+        if (std::isfinite(S.km[2 * i])) S.k = std::max(S.k, S.km[2 * i]);
     S.a.resize(nodes.size());
     S.b.resize(nodes.size());
     for (size_t i = 0; i < nodes.size(); ++i) {
         const rtw_bvh_node& n = nodes[i];
-        const uint32_t kmb = (bf16_up(S.km[2 * i]) << 16) | bf16_up(S.km[2 * i + 1]);
+        const float m = std::isfinite(S.km[2 * i]) ? S.km[2 * i + 1] : std::numeric_limits<float>::infinity();
         S.a[i] = make_float4(n.min[0], n.min[1], n.min[2], n.max[0]);
-        S.b[i] = make_float4(n.max[1], n.max[2], ibits(kids(n)), ibits((int32_t)kmb));
+        S.b[i] = plain_spheres ? make_float4(n.max[1], n.max[2], ibits(kids(n)), m)
+                               : make_float4(n.max[1], n.max[2], ibits((int32_t)((uint32_t)n.left << 2) | n.axis),
+                                             ibits(n.right));
     }
-    // plain-sphere worlds walk two children per step with the root's children word as the first lane state
     S.root_c2 = kids(nodes[(size_t)S.root]);
     S.box.resize((size_t)L * 2);
     for (int32_t i = 0; i < L; ++i) {
@@ -3037,9 +3118,10 @@ struct rtw_gpu_world {
     DWorld w{};
     const DWorld* wdev = nullptr;
     int32_t node_count = 0, leaf_count = 0, depth = 1;
-    int32_t tri_count = 0, rect_count = 0, material_count = 0, texture_count = 0;
+    int32_t tri_count = 0, rect_count = 0, material_count = 0, texture_count = 0, sphere_count = 0, box_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int32_t sah_nodes = 0;  // nodes of the SAH tree, 0: the world takes the reference tree only (§5.6)
+    bool sah_folded = false;  // its node records are the two-children walk's (plain-sphere worlds)
     int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
     int32_t tex_kinds = TX_ANY;   // TX_*: the texture code the world's textures need
     int cus = 0;
@@ -3253,6 +3335,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     const SahTables sah = build_sah_tables(w);
     const size_t o_sa = sah.ok ? L.push(sah.a.data(), sah.a.size() * sizeof(float4)) : 0;
     const size_t o_sb = sah.ok ? L.push(sah.b.data(), sah.b.size() * sizeof(float4)) : 0;
+    const size_t o_sk = sah.ok && !sah.folded ? L.push(sah.km.data(), sah.km.size() * sizeof(float)) : 0;
     const size_t o_lb = sah.ok ? L.push(sah.box.data(), sah.box.size() * sizeof(float4)) : 0;
     const size_t o_lk = sah.ok && !sah.key.empty() ? L.push(sah.key.data(), sah.key.size() * sizeof(uint4)) : 0;
 
@@ -3307,6 +3390,8 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         d.leaf_key = o_lk ? (const uint4*)(base + o_lk) : nullptr;
         d.sah_root = sah.root;
         d.sah_root_c2 = sah.root_c2;
+        d.sah_k = sah.k;
+        d.sah_km = sah.folded ? nullptr : (const float2*)(base + o_sk);
     }
     d.has_light = w->has_light;
     d.wc = (const WorldConst*)(base + o_wc);
@@ -3322,10 +3407,13 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     g->depth = std::max(1, depth);
     if (sah.ok) {
         g->sah_nodes = (int32_t)sah.a.size();
+        g->sah_folded = sah.folded;
         g->depth = std::max(g->depth, sah.depth);
     }
     g->tri_count = w->triangle_count;
     g->rect_count = w->rect_count;
+    g->sphere_count = w->sphere_count;
+    g->box_count = w->box_count;
     g->material_count = w->material_count;
     g->texture_count = w->texture_count;
     g->mk_world = 1;
@@ -3390,10 +3478,15 @@ extern "C" RTW_API int rtw_debug_sah_tree(const rtw_world* w, double* out) {
     };
     // measured over the subtree of the root's internal child when the other child is a leaf (suzanne's
     // ground sphere would otherwise make every mesh node's area vanish against the root's)
+    // a node's children in either record format (build_sah_tables)
+    auto kids = [&](int32_t i, int c) {
+        const int32_t kb = (int32_t)fbits(S.b[(size_t)i].z);
+        if (!S.folded) return c ? (int32_t)fbits(S.b[(size_t)i].w) : kb >> 2;
+        return c ? kb >> 17 : (int32_t)((uint32_t)kb << 15) >> 17;
+    };
     int32_t root = S.root;
     if (root >= 0) {
-        const int32_t kb = (int32_t)fbits(S.b[(size_t)root].z);
-        const int32_t l = (int32_t)((uint32_t)kb << 15) >> 17, r = kb >> 17;
+        const int32_t l = kids(root, 0), r = kids(root, 1);
         if ((l < 0) != (r < 0)) root = l >= 0 ? l : r;
     }
     double nodes = 1.0, leaves = 0.0;  // the top node's test; a child is tested when its parent passes
@@ -3405,8 +3498,7 @@ extern "C" RTW_API int rtw_debug_sah_tree(const rtw_world* w, double* out) {
             todo.pop_back();
             const double an = area(S.a[(size_t)i], S.b[(size_t)i]) / ar;
             for (int c = 0; c < 2; ++c) {
-                const int32_t kb = (int32_t)fbits(S.b[(size_t)i].z);
-                const int32_t ch = c ? kb >> 17 : (int32_t)((uint32_t)kb << 15) >> 17;
+                const int32_t ch = kids(i, c);
                 (ch < 0 ? leaves : nodes) += an;
                 if (ch >= 0) todo.push_back(ch);
             }
@@ -3421,10 +3513,6 @@ extern "C" RTW_API int rtw_debug_sah_tree(const rtw_world* w, double* out) {
     // first, until 4): steps, box tests, leaf tests, all per ray by the area measure
     if (root >= 0) {
         const double ar = area(S.a[(size_t)root], S.b[(size_t)root]);
-        auto kids = [&](int32_t i, int c) {
-            const int32_t kb = (int32_t)fbits(S.b[(size_t)i].z);
-            return c ? kb >> 17 : (int32_t)((uint32_t)kb << 15) >> 17;
-        };
         double st2 = 0.0, bx2 = 0.0, st4 = 0.0, bx4 = 0.0, lf4 = 0.0;
         std::vector<int32_t> todo{root};
         while (!todo.empty()) {
@@ -3565,8 +3653,11 @@ int make_args(const rtw_gpu_world* g, const rtw_render_params* p, KArgs& A) {
     A.tri_count = g->tri_count;
     A.rect_count = g->rect_count;
     A.material_count = g->material_count;
+    A.sphere_count = g->sphere_count;
+    A.box_count = g->box_count;
     A.texture_count = g->texture_count;
     A.sh_li = A.sh_mat = A.sh_tex0 = A.sh_box = -1;
+    A.sh_xf = A.sh_sph = A.sh_bx = A.sh_rect = -1;
     A.queue = g->queue;
     A.wdev = g->wdev;
     A.trace_min = 32;
@@ -3593,7 +3684,10 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     if (const char* e = std::getenv("RTW_LEAF_KINDS")) lk = std::max(lk, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RTW_TEX_KINDS")) tx = std::max(tx, std::min(1, std::atoi(e)));
     // the SAH tree (§5.6) replaces the reference tree in LDS; the counting variant keeps the latter
-    const bool sah = (!stats || ktree) && g->sah_nodes > 0 && g->mk_world && lk <= LK_WRAPPED;
+    // (a plain-sphere world's SAH records are the two-children walk's: another leaf-kind loop, forced by
+    // RTW_LEAF_KINDS, takes the reference tree)
+    const bool sah = (!stats || ktree) && g->sah_nodes > 0 && g->mk_world && lk <= LK_WRAPPED &&
+                     g->sah_folded == (lk == LK_SPHERES);
     A.sah = sah ? 1 : 0;
     // the drain's cooperative trace (coop_trace): worlds small enough to test every leaf per ray
     A.coop_max = g->leaf_count <= RTW_COOP_LEAVES ? (int32_t)env_size("RTW_COOP_MAX", RTW_COOP_MAX) : 0;
@@ -3619,16 +3713,18 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     // LDS scene: [node_a n][node_b n][leaf records L][cull constants (n + 1) / 2, reference tree only][rects
     // 2R] (+ the triangle records in mode 2)
     const size_t scene_bytes =
-        (size_t)(2 * A.node_count + g->leaf_count + (sah ? 0 : (A.node_count + 1) / 2) + 2 * g->rect_count) * sizeof(float4);
+        (size_t)(2 * A.node_count + g->leaf_count + (sah && lk == LK_SPHERES ? 0 : (A.node_count + 1) / 2) +
+                 2 * g->rect_count) * sizeof(float4);
     A.fast_off = 2 * A.node_count;
     int mode = 0;
-    if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && g->leaf_count < 32768 &&
-        A.node_count < 32768 &&
-        g->node_count < 32768 && scene_bytes + tri_bytes + stack16_bytes <= cap)
+    // 16-bit stack entries (traverse's StackEntry): worlds of < 2^15 nodes (both trees) and leaves
+    const bool small = g->leaf_count < 32768 && A.node_count < 32768 && g->node_count < 32768;
+    const size_t stack1_bytes = lk != LK_SPHERES ? stack16_bytes : stack_bytes;  // mode 1
+    if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && small && scene_bytes + tri_bytes + stack16_bytes <= cap)
         mode = 2;
-    else if (scene_bytes + stack_bytes <= cap) mode = 1;
+    else if (scene_bytes + stack1_bytes <= cap && (small || lk == LK_SPHERES)) mode = 1;
     if (lds_mode_env) mode = std::min(mode, std::atoi(lds_mode_env));
-    size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes + stack16_bytes : stack_bytes);
+    size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes + stack16_bytes : mode == 1 ? stack1_bytes : stack_bytes);
     // shading tables after the scene when they fit too (RTW_NO_SHADE_LDS=1: keep them in HBM / L2)
     const int32_t scene_f4 = (int32_t)((scene_bytes + (mode == 2 ? tri_bytes : 0)) / sizeof(float4));
     const size_t sh_bytes = (size_t)(g->leaf_count + A.material_count + (tx == TX_SOLID ? A.texture_count : 0)) * sizeof(int4);
@@ -3649,6 +3745,19 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         A.stack_off += (int32_t)(box_bytes / sizeof(float4));
         lds += box_bytes;
     }
+    // ... and the generic leaf path's transforms, spheres and boxes (worlds with wrapped or box leaves, or
+    // volumes; RTW_NO_GEN_LDS=1 keeps them in HBM / L2)
+    A.sh_xf = A.sh_sph = A.sh_bx = -1;
+    A.sh_rect = mode >= 1 ? 2 * A.node_count + g->leaf_count + (sah && lk == LK_SPHERES ? 0 : (A.node_count + 1) / 2) : -1;
+    const size_t gen_bytes = (size_t)(3 * g->leaf_count + g->sphere_count + 2 * g->box_count) * sizeof(float4);
+    const char* ngl = std::getenv("RTW_NO_GEN_LDS");
+    if (sh && lk >= LK_WRAPPED && lds + gen_bytes <= cap && !(ngl && ngl[0] && ngl[0] != '0')) {
+        A.sh_xf = A.stack_off;
+        A.sh_sph = A.sh_xf + 3 * g->leaf_count;
+        A.sh_bx = A.sh_sph + g->sphere_count;
+        A.stack_off += (int32_t)(gen_bytes / sizeof(float4));
+        lds += gen_bytes;
+    }
     using KFn = void (*)(KArgs);
 #define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}
     static const KFn fns[2][5][3] = {
@@ -3663,7 +3772,16 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     static const KFn fns_stats_sah[4][3] = {RTW_SSET(LK_SPHERES), RTW_SSET(LK_TRIS), RTW_SSET(LK_PLAIN),
                                             RTW_SSET(LK_WRAPPED)};
 #undef RTW_SSET
-    const KFn kf = stats ? (sah ? fns_stats_sah[lk][mode] : fns_stats[mode]) : fns[tx][lk][mode];
+    // worlds whose generic leaf tables are in LDS: the GEN variants (leaf kinds 3 and 4, LDS modes 1 and 2)
+    static const KFn fns_gen[2][2][2] = {
+        {{render_kernel<false, 1, LK_WRAPPED, TX_SOLID, true>, render_kernel<false, 2, LK_WRAPPED, TX_SOLID, true>},
+         {render_kernel<false, 1, LK_ANY, TX_SOLID, true>, render_kernel<false, 2, LK_ANY, TX_SOLID, true>}},
+        {{render_kernel<false, 1, LK_WRAPPED, TX_ANY, true>, render_kernel<false, 2, LK_WRAPPED, TX_ANY, true>},
+         {render_kernel<false, 1, LK_ANY, TX_ANY, true>, render_kernel<false, 2, LK_ANY, TX_ANY, true>}}};
+    const bool gen = !stats && A.sh_xf >= 0;  // (the counting variant reads the HBM copies)
+    const KFn kf = stats ? (sah ? fns_stats_sah[lk][mode] : fns_stats[mode])
+                 : gen   ? fns_gen[tx][lk - LK_WRAPPED][mode - 1]
+                         : fns[tx][lk][mode];
     if (!stats) {
         g->last_kernel[0] = mode;
         g->last_kernel[1] = lk;

@@ -9,6 +9,7 @@
 #   kt                rocprofv3 kernel-trace summary of the headline bench command -> kt/
 #   part8[:SCENES]    one rank's share of 8-way splits (tools/part_bench.py), default final_scene1,suzanne
 #   pmc:SCENE[:W:H:SPP]  the PMC counter passes of tools/gpu_pmc3.sh for one scene
+#   py:SCRIPT[,ARGS]  python SCRIPT ARGS (commas become spaces) -> py_<n>.txt
 #   ab:SCENES:REPS:CASE1;CASE2..  tools/ab_mix.sh (cases "<variant>|<env>"; SCENES comma-separated);
 #                     AB_ARGS passes extra bench.py arguments
 set -o pipefail
@@ -16,6 +17,7 @@ O=gpurun_out/${TAG:-run}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 nb=0
 nf=0
+np_=0
 for step in "$@"; do
   kind=${step%%:*}; rest=${step#*:}; [ "$rest" = "$step" ] && rest=""
   echo "== $step ($(date +%T))" | tee -a $O/steps.log
@@ -45,6 +47,9 @@ for step in "$@"; do
     pmc)
       IFS=: read -r sc w h spp <<< "$rest"
       SCENE=$sc W=${w:-1920} H=${h:-1080} SPP=${spp:-32} PMC_OUT=$O/pmc_$sc bash tools/gpu_pmc3.sh || exit 1 ;;
+    py)
+      np_=$((np_ + 1))
+      timeout -k 10 900 python ${rest//,/ } > $O/py_$np_.txt 2>&1 || { tail -20 $O/py_$np_.txt; exit 1; } ;;
     ab)
       IFS=: read -r sc reps cases <<< "$rest"
       IFS=';' read -r -a C <<< "$cases"
