@@ -2170,7 +2170,9 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         const uint32_t wi = rel - g * A.fd_rank.d;
                         ck = fdiv(wi, A.fd_tile);
                         it = wi - ck * A.fd_tile.d;
-                        lt = A.tile_perm[g];  // (a per-lane cache of it: -0.3 %, profiles/r04/v9_proof_lds_ab.txt)
+                        // (a per-lane cache of it: -0.3 %, profiles/r04/v9_proof_lds_ab.txt; the reserve's tiles
+                        // read at batch fetch, a wave-uniform cache: within noise, profiles/r05/ab_r5i.txt)
+                        lt = A.tile_perm[g];
                         c = lt * A.fd_tile.d + it;
                     } else {  // chunk-major: pass after pass over the slots
                         ck = fdiv(rel, A.fd_total);

@@ -9,6 +9,7 @@
 #   kt                rocprofv3 kernel-trace summary of the headline bench command -> kt/
 #   part8[:SCENES]    one rank's share of 8-way splits (tools/part_bench.py), default final_scene1,suzanne
 #   pmc:SCENE[:W:H:SPP]  the PMC counter passes of tools/gpu_pmc3.sh for one scene
+#   env:VAR=VALUE / unenv:VAR  set / unset an environment variable for the steps that follow
 #   py:SCRIPT[,ARGS]  python SCRIPT ARGS (commas become spaces) -> py_<n>.txt
 #   ab:SCENES:REPS:CASE1;CASE2..  tools/ab_mix.sh (cases "<variant>|<env>"; SCENES comma-separated);
 #                     AB_ARGS passes extra bench.py arguments
@@ -47,6 +48,10 @@ for step in "$@"; do
     pmc)
       IFS=: read -r sc w h spp <<< "$rest"
       SCENE=$sc W=${w:-1920} H=${h:-1080} SPP=${spp:-32} PMC_OUT=$O/pmc_$sc bash tools/gpu_pmc3.sh || exit 1 ;;
+    env)
+      export "$rest" ;;  # for the steps that follow, e.g. env:RTW_COOP_MAX=8
+    unenv)
+      unset "$rest" ;;
     py)
       np_=$((np_ + 1))
       timeout -k 10 900 python ${rest//,/ } > $O/py_$np_.txt 2>&1 || { tail -20 $O/py_$np_.txt; exit 1; } ;;
