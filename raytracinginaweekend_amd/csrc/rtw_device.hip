@@ -94,7 +94,8 @@ struct DWorld {
     const float4* node_b;  // {max.y, max.z, bits(left << 2 | axis), bits(right)}
     const float2* node_km; // proximity-cull constants {k, m} (rtw_cull.h)
     const int4* leaf_info; // {geom_kind, geom_index, material, flags}
-    const float4* leaf_fast; // plain sphere: {center.xyz, radius}; else w = NaN, x = bits(1) for a plain triangle (y = index)
+    const float4* leaf_fast; // plain sphere: {center.xyz, radius}; else w = NaN, x = a tag (1 plain triangle, 2 plain
+                             // rect, 3 animated plain sphere, 0 other) and y = the primitive's index
     const float4* leaf_xf; // 3 per leaf: {neg_inv_density, off.xyz}, {ys, yc, vel.x, vel.y}, {vel.z,0,0,0}
     const float4* spheres; // {center.xyz, radius}
     const float4* rects;   // 2 per rect: {dist, r0.0, r0.1, r1.0}, {r1.1, bits(plane), 0, 0}
@@ -1643,6 +1644,14 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB
             if (tri_test(LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), T.ray, 0.001f,
                          T.te, t))
                 take(t, leaf);
+        } else if (LK >= LK_WRAPPED && __float_as_int(sph.x) == 3) {
+            // a sphere under an Animation wrapper only (C5's moving spheres): the generic path's
+            // arithmetic (leaf_t: the ray moved by -velocity x time, hittable.rs:239-244, then the sphere
+            // test) without its leaf-record read and kind dispatch
+            if (STATS) st.c[ST_T_SPHERE]++;
+            const Ray rr = xf_reverse(anim_xf(w, S, leaf, T.ray.time), T.ray);
+            float t;
+            if (sphere_t(tab_gen(S, S.sph, w.spheres, __float_as_int(sph.y)), rr, 0.001f, T.te, t)) take(t, leaf);
         } else if (LK >= LK_WRAPPED) {
             float t;
             if (leaf_t<STATS, LK == LK_ANY>(w, S, leaf, T.ray, 0.001f, T.te, T.rng, t, st)) take(t, leaf);
@@ -3235,7 +3244,12 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
             lf[(size_t)i] = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius);
         } else {
             // w = NaN: not a plain sphere; x = 1 tags a plain triangle, 2 a plain rect (index in y)
-            const int tag = l.flags != 0 ? 0 : (l.geom_kind == RTW_GEOM_TRIANGLE ? 1 : (l.geom_kind == RTW_GEOM_RECT ? 2 : 0));
+            // (3: a sphere under an Animation wrapper only, the traversal's fast path for it)
+            const int tag = l.flags == RTW_LEAF_ANIMATION && l.geom_kind == RTW_GEOM_SPHERE ? 3
+                            : l.flags != 0                     ? 0
+                            : l.geom_kind == RTW_GEOM_TRIANGLE ? 1
+                            : l.geom_kind == RTW_GEOM_RECT     ? 2
+                                                               : 0;
             lf[(size_t)i] = make_float4(ibits(tag), ibits(l.geom_index), 0.0f, ibits(0x7FC00000));
         }
     }
