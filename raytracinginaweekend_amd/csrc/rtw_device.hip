@@ -12,7 +12,7 @@
 //   alone, then proven to be the reference DFS's answer (hittable.rs:429-473) with one slab test on
 //   the leaf's parent box in the reference tree; rays the proof does not cover are re-traced on the
 //   reference tree in the reference's order (near child first by ray.direction[axis] > 0, both
-//   children, te shrinking).  Ties are resolved by the leaves' reference DFS keys (coop_trace).
+//   children, te shrinking).  Ties are resolved by the leaves' reference DFS keys (coop_solve).
 //   Candidate tests compute only `t`; the hit record is rebuilt once for the closest leaf -- a pure
 //   function of (leaf, ray, t).  Volumes draw their RNG during traversal in the reference's order
 //   (their worlds keep the reference tree).
@@ -81,6 +81,7 @@
 #ifndef RTW_LDS_SCENE_MAX
 #define RTW_COOP_MAX 32      // drain: live lanes at most for the wave-cooperative trace (RTW_COOP_MAX=0: off); 4: suzanne -1.1 %, its 8-way shares up to 64.5 ms against 59.4 (profiles/r04/v3_experiments_ab.txt, v4_...)
 #define RTW_COOP_LEAVES 4096 // ... in worlds of at most this many leaves
+#define RTW_MB_POLLS (1u << 22)  // a finished wave's polls for the block's posted drain rays, at most (mb_slot)
 #define RTW_LDS_SCENE_MAX (160 * 1024)  // LDS bytes per block the scene (+ stack) may take
 #endif
 
@@ -120,7 +121,7 @@ struct DWorld {
     const float4* sah_b;
     const float2* sah_km;
     const float4* leaf_box;
-    // each leaf's place in the reference tree's DFS (coop_trace's tie resolution): {side bits, and
+    // each leaf's place in the reference tree's DFS (coop_solve's tie resolution): {side bits, and
     // per axis the bits of the ancestors splitting on it}, bit 31 - k for the ancestor at depth k;
     // null when the reference tree is deeper than 32
     const uint4* leaf_key;
@@ -223,8 +224,8 @@ struct KArgs {
     int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
                               // re-traced on the reference tree where the proof does not hold (§5.6)
     int32_t coop_max;         // drain: a wave with at most this many live lanes traces each ray with all
-                              // 64 lanes over every leaf (coop_trace); 0: never
-    int32_t coop_ties;        // 1: the walk's tied rays are resolved by coop_trace (else re-traced); 2: audit
+                              // 64 lanes over every leaf (coop_solve); 0: never
+    int32_t coop_ties;        // 1: the walk's tied rays are resolved by coop_solve (else re-traced); 2: audit
     uint64_t tune_items;      // items per tuning epoch (0: this launch does not explore)
     // 1: a work item is a whole pixel (all spp samples of a slot, one lane, in sample order): the lane
     // sums the colours in registers -- the reference's sequential .sum(), rendering.rs:172-179 -- and
@@ -246,6 +247,9 @@ struct KArgs {
     // (3 per leaf), spheres, boxes (2 per box); and the rects of the LDS scene
     int32_t sh_xf, sh_sph, sh_bx, sh_rect;
     int32_t sphere_count, box_count;
+    // the drain's shared cooperative trace (mb_slot): the block's mailbox words in LDS (float4 offset,
+    // -1: each wave traces its own drained rays), and the rays one wave's stack columns hold
+    int32_t mb_off, mb_cap;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -1499,7 +1503,7 @@ __device__ unsigned long long rtw_wave_extra[8 * 8192];
 
 // PH_REF: the ray is traced on the reference tree (the SAH path's fallback, §5.6)
 // PH_DONE: the queues are empty and the lane's last path is finished (it stays in the loop, masked
-// by its phase, so that the wave's remaining rays can be traced with all 64 lanes: coop_trace)
+// by its phase, so that the wave's remaining rays can be traced with all 64 lanes: coop_solve)
 enum { PH_PIXEL = 0, PH_TRACE = 1, PH_SHADE = 2, PH_REF = 3, PH_DONE = 4 };
 // traversal modes: the reference tree (DFS of hittable.rs:429-473 with hit_cond AND the cull), the
 // SAH tree (cull only, closest hit with ties flagged), the reference tree for PH_REF lanes with
@@ -1675,7 +1679,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB
         // (rare lanes) runs to the end
         if (TM != TM_FALLBACK && (uint32_t)__popcll(tr) < (uint32_t)trace_min && __ballot(T.phase == PH_SHADE) != 0)
             break;
-        // the drain: the last few tracing lanes (the long walks) go to coop_trace
+        // the drain: the last few tracing lanes (the long walks) go to coop_solve
         if (TM == TM_SAH && (int32_t)__popcll(tr) <= coop_exit) break;
         if (STATS) {
             const unsigned long long lm = __ballot(T.phase == ACT && T.node < 0);
@@ -1823,10 +1827,22 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB
 // decides as for any hit; a lane holding two tied leaves keeps the flag (re-traced on the reference
 // tree).  Rays of `todo` only (SAH rays: RTW_TF_SAH).  `audit` (tests only, RTW_COOP_AUDIT=1) takes
 // the DFS-last tied leaf instead: wrong images, which shows that the resolution decides them.
+// one ray of the cooperative trace, the same in every lane
+struct CRay {
+    Ray r;
+    V3 inv;
+    int32_t sgn;  // Trav.fast: bits 0-2 ray.d[axis] > 0
+};
+// the wave's answer for it (wave-uniform): the closest leaf (-1: none), te = succ(its t) as take()
+// leaves it, and whether the tie flag stays
+struct CHit {
+    int32_t found;
+    float te;
+    bool tie;
+};
 template <int LDS, int LK>
-__device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T, unsigned long long todo, int32_t n_nodes,
-                                        int32_t n_leaves, int32_t n_rects, int32_t fast_off, bool audit) {
-    const DWorld& w = *wp;
+__device__ __forceinline__ CHit coop_solve(const DWorld& w, const CRay& a, int32_t n_nodes, int32_t n_leaves,
+                                           int32_t n_rects, int32_t fast_off, bool audit) {
     constexpr bool LDS_SCENE = LDS >= 1;
     // the SAH tree's LDS scene: plain-sphere worlds have no cull-constant section
     const int32_t rect_off = 2 * n_nodes + n_leaves + (LK == LK_SPHERES ? 0 : (n_nodes + 1) / 2);
@@ -1836,108 +1852,146 @@ __device__ __forceinline__ Trav coop_trace(const DWorld* __restrict__ wp, Trav T
     const float4* fast = LDS_SCENE ? smem + fast_off : uniform_ptr(w.leaf_fast);
     const int lane = threadIdx.x & 63;
     const uint4* keys = uniform_ptr(w.leaf_key);
-    // one ray's state in the cooperative trace (each lane's best leaf so far, and how many of its
-    // leaves reported exactly that t)
-    struct CRay {
-        Ray r;
-        V3 inv;
-        int32_t sgn;  // bits 0-2: ray.d[axis] > 0
-        float best;
-        int32_t bl;
-        uint32_t cnt;
-    };
-    auto load_ray = [&](int src) {
-        CRay c;
-        c.r.o = v3(__shfl(T.ray.o.x, src), __shfl(T.ray.o.y, src), __shfl(T.ray.o.z, src));
-        c.r.d = v3(__shfl(T.ray.d.x, src), __shfl(T.ray.d.y, src), __shfl(T.ray.d.z, src));
-        c.r.time = __shfl(T.ray.time, src);
-        c.inv = v3(__shfl(T.inv.x, src), __shfl(T.inv.y, src), __shfl(T.inv.z, src));
-        c.sgn = __shfl(T.fast, src);
-        c.best = F32_INF;
-        c.bl = -1;
-        c.cnt = 0;
-        return c;
-    };
-    auto keep = [](CRay& c, bool hit, float t, int32_t leaf) {
+    // each lane's best leaf so far, and how many of its leaves reported exactly that t
+    float best = F32_INF;
+    int32_t bl = -1;
+    uint32_t cnt = 0;
+    auto keep = [&](bool hit, float t, int32_t leaf) {
         if (hit) {
-            c.cnt = t == c.best ? c.cnt + 1 : t < c.best ? 1u : c.cnt;
-            c.bl = t < c.best ? leaf : c.bl;
-            c.best = t < c.best ? t : c.best;
-        }
-    };
-    // the wave's answer for ray c: the smallest root, its leaf, the tie resolution; written to lane src
-    auto finish = [&](const CRay& c, int src) {
-        float m = c.best;
-#pragma unroll
-        for (int k = 1; k < 64; k <<= 1) m = rtw_minr(m, __shfl_xor(m, k));
-        const unsigned long long at = __ballot(c.bl >= 0 && c.best == m);
-        bool tie = __ballot(c.bl >= 0 && c.best == m && c.cnt >= 2) != 0;
-        int win = at ? __ffsll((long long)at) - 1 : 0;
-        if (__popcll(at) >= 2) {  // one tied leaf per lane: the first in the reference's DFS order
-            if (keys) {
-                uint32_t k = 0xFFFFFFFFu;
-                if ((at >> lane) & 1) {
-                    const uint4 q = keys[c.bl];
-                    // bit = side XOR (the right child is visited first: ray.d[axis] <= 0)
-                    k = q.x ^ ((c.sgn & 1) ? 0u : q.y) ^ ((c.sgn & 2) ? 0u : q.z) ^ ((c.sgn & 4) ? 0u : q.w);
-                    if (audit) k = ~k;
-                }
-                uint32_t km = k;
-#pragma unroll
-                for (int j = 1; j < 64; j <<= 1) km = min(km, (uint32_t)__shfl_xor((int)km, j));
-                win = __ffsll((long long)__ballot(((at >> lane) & 1) && k == km)) - 1;
-            } else {
-                tie = true;
-            }
-        }
-        const int32_t found = at ? __shfl(c.bl, win) : -1;
-        if (lane == src) {
-            T.found = found;
-            T.te = found >= 0 ? __int_as_float(__float_as_int(m) + 1) : F32_INF;  // succ(t), as take()
-            T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
-            T.sp = 0;
-            T.phase = PH_SHADE;
+            cnt = t == best ? cnt + 1 : t < best ? 1u : cnt;
+            bl = t < best ? leaf : bl;
+            best = t < best ? t : best;
         }
     };
     // a leaf's first root in [ts, te) with te = succ(the lane's best so far): a root beyond the lane's best
     // cannot change the lane's answer, and one equal to it still counts (ties); the triangle test then
-    // stops at t for most leaves and reads its record's second half only for closer ones (the drain's
-    // waves read every record of every leaf per ray: LDS-bound)
-    auto te_of = [](const CRay& c) {
-        return c.best < F32_INF ? __int_as_float(__float_as_int(c.best) + 1) : F32_INF;
-    };
+    // stops at t for most leaves and reads its record's second half only for closer ones
     // (two rays per pass over the leaves, sharing the record reads, lost 2.4 % on suzanne and 3.7 % on
     // cornell_cube to spills: profiles/r04/v10_coop_ab.txt)
-    while (todo) {  // wave-uniform: one ray at a time
-        const int s1 = __ffsll((long long)todo) - 1;
-        todo &= todo - 1;
-        CRay a = load_ray(s1);
-        // software-pipelined: the next leaf record is read before this leaf's test, so that its LDS
-        // latency overlaps the triangle / rect record read that depends on this one (one round trip per
-        // leaf instead of two; the drain's rays are latency-bound)
-        float4 sph_n = lane < n_leaves ? fast[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        for (int32_t leaf = lane; leaf < n_leaves; leaf += 64) {
-            const float4 sph = sph_n;
-            if (leaf + 64 < n_leaves) sph_n = fast[leaf + 64];
-            float t;
-            const float te = te_of(a);
-            if (LK == LK_SPHERES || sph.w == sph.w) {
-                keep(a, sphere_t(sph, a.r, 0.001f, te, t), t, leaf);
-            } else if (LK >= LK_PLAIN && __float_as_int(sph.x) == 2) {
-                const int ri = __float_as_int(sph.y);
-                const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
-                const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
-                keep(a, rect_t_mk(g, a.r, a.inv, 0.001f, te, t), t, leaf);  // SAH rays are Markstein-exact
-            } else {
-                const int ti = __float_as_int(sph.y);
-                keep(a, tri_test(LDS == 2 ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), a.r,
-                                 0.001f, te, t),
-                     t, leaf);
-            }
+    // software-pipelined: the next leaf record is read before this leaf's test, so that its LDS
+    // latency overlaps the triangle / rect record read that depends on this one (one round trip per
+    // leaf instead of two; the drain's rays are latency-bound)
+    float4 sph_n = lane < n_leaves ? fast[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int32_t leaf = lane; leaf < n_leaves; leaf += 64) {
+        const float4 sph = sph_n;
+        if (leaf + 64 < n_leaves) sph_n = fast[leaf + 64];
+        float t;
+        const float te = best < F32_INF ? __int_as_float(__float_as_int(best) + 1) : F32_INF;
+        if (LK == LK_SPHERES || sph.w == sph.w) {
+            keep(sphere_t(sph, a.r, 0.001f, te, t), t, leaf);
+        } else if (LK >= LK_PLAIN && __float_as_int(sph.x) == 2) {
+            const int ri = __float_as_int(sph.y);
+            const float4 ra = rects[2 * ri], rb = rects[2 * ri + 1];
+            const RectG g{__float_as_int(rb.y), ra.x, ra.y, ra.z, ra.w, rb.x};
+            keep(rect_t_mk(g, a.r, a.inv, 0.001f, te, t), t, leaf);  // SAH rays are Markstein-exact
+        } else {
+            const int ti = __float_as_int(sph.y);
+            keep(tri_test(LDS == 2 ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), a.r, 0.001f, te, t), t,
+                 leaf);
         }
-        finish(a, s1);
     }
-    return T;
+    // the wave's answer: the smallest root, its leaf, the tie resolution
+    float m = best;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) m = rtw_minr(m, __shfl_xor(m, k));
+    const unsigned long long at = __ballot(bl >= 0 && best == m);
+    bool tie = __ballot(bl >= 0 && best == m && cnt >= 2) != 0;
+    int win = at ? __ffsll((long long)at) - 1 : 0;
+    if (__popcll(at) >= 2) {  // one tied leaf per lane: the first in the reference's DFS order
+        if (keys) {
+            uint32_t k = 0xFFFFFFFFu;
+            if ((at >> lane) & 1) {
+                const uint4 q = keys[bl];
+                // bit = side XOR (the right child is visited first: ray.d[axis] <= 0)
+                k = q.x ^ ((a.sgn & 1) ? 0u : q.y) ^ ((a.sgn & 2) ? 0u : q.z) ^ ((a.sgn & 4) ? 0u : q.w);
+                if (audit) k = ~k;
+            }
+            uint32_t km = k;
+#pragma unroll
+            for (int j = 1; j < 64; j <<= 1) km = min(km, (uint32_t)__shfl_xor((int)km, j));
+            win = __ffsll((long long)__ballot(((at >> lane) & 1) && k == km)) - 1;
+        } else {
+            tie = true;
+        }
+    }
+    CHit h;
+    h.found = at ? __shfl(bl, win) : -1;
+    h.te = h.found >= 0 ? __int_as_float(__float_as_int(m) + 1) : F32_INF;
+    h.tie = tie;
+    return h;
+}
+// a lane's traversal state after coop_solve answered its ray
+__device__ __forceinline__ void coop_apply(Trav& T, int32_t found, float te, bool tie) {
+    T.found = found;
+    T.te = te;
+    T.fast = tie ? (T.fast | RTW_TF_TIE) : (T.fast & ~RTW_TF_TIE);
+    T.sp = 0;
+    T.phase = PH_SHADE;
+}
+// The drain shared by the block's waves (§5.7).  coop_solve alone leaves each wave with its own
+// drained rays: one wave of a block may still trace hundreds of them (suzanne's 8-GPU shares: up to
+// 6.7 ms after the queues ran dry) while its 15 neighbours have finished.  Instead, a wave whose lanes
+// all trace in the drain posts its rays to a mailbox in LDS; the owner traces the posts nobody has taken
+// yet (from its own lanes), and every wave of the block with no live lane left (a helper, after the
+// main loop) takes posted rays and traces them (from the posts) -- both with coop_solve, one answer each.
+// Mailbox of wave v: state[v] = gen << 16 | total << 8 | next (rays [next, total) not yet taken; a
+// take is a CAS next -> next + 1), done[v] counts the answered rays, and `live` the block's waves that
+// still have a live lane.  The rays themselves sit in the owner's traversal-stack columns (free then:
+// no lane of the wave is inside a walk), 64 B each: {o, time} {d, fast bits} {inv, -} {answer}.
+// Progress: a helper never waits while holding a taken ray, the owner waits only for rays taken by
+// others, and a helper leaves once `live` is 0 (each wave decrements it once, on its way to helping).
+#define RTW_MB_WORDS 36  // state[16], done[16], live (9 float4)
+template <int LDS, int LK>
+__device__ __forceinline__ float4* mb_slot(int32_t stack_off, int v, int j) {
+    // the stack's entry size (traverse's StackEntry): a wave's 64 entries of one level hold ES rays
+    constexpr int ES = (LDS == 2 || (LDS == 1 && LK != LK_SPHERES)) ? 2 : 4;
+    return smem + stack_off + (j / ES) * (RTW_BLOCK * ES / 16) + v * (64 * ES / 16) + (j % ES) * 4;
+}
+// the owner's take of its own next post (wave-uniform); false: all taken
+__device__ __forceinline__ bool mb_take_own(uint32_t* mb, int v, int& j) {
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        const uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(&mb[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if ((s & 0xFFu) >= ((s >> 8) & 0xFFu)) return false;
+        uint32_t expect = s;
+        bool ok = false;
+        if (lane == 0)
+            ok = __hip_atomic_compare_exchange_strong(&mb[v], &expect, s + 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane((int)ok)) {
+            j = (int)(s & 0xFFu);
+            return true;
+        }
+    }
+}
+// a post's answer (one lane): into its slot, then counted (release)
+__device__ __forceinline__ void mb_answer(uint32_t* mb, float4* q, int u, const CHit& h) {
+    q[3] = make_float4(__int_as_float(h.found), h.te, h.tie ? 1.0f : 0.0f, 0.0f);
+    __hip_atomic_fetch_add(&mb[16 + u], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// one wave-uniform take: the first mailbox from wave v0 on with a ray not yet taken; -1: none
+__device__ __forceinline__ int mb_take(uint32_t* mb, int v0, int& j) {
+    const int lane = threadIdx.x & 63;
+    constexpr int NW = RTW_BLOCK / 64;
+    for (;;) {
+        const int u = (v0 + lane) % NW;
+        const uint32_t s = lane < NW ? __hip_atomic_load(&mb[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+        const unsigned long long open = __ballot(lane < NW && (s & 0xFFu) < ((s >> 8) & 0xFFu));
+        if (open == 0) return -1;
+        const int i = __ffsll((long long)open) - 1;
+        const int uu = (v0 + i) % NW;
+        const uint32_t si = (uint32_t)__builtin_amdgcn_readlane((int)s, i);
+        uint32_t expect = si;
+        bool ok = false;
+        if (lane == 0)
+            ok = __hip_atomic_compare_exchange_strong(&mb[uu], &expect, si + 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane((int)ok)) {
+            j = (int)(si & 0xFFu);
+            return uu;
+        }
+    }
 }
 
 template <bool STATS, int LDS, int LK, int TX, bool GEN>
@@ -1988,6 +2042,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
             }
         }
+        if (A.mb_off >= 0 && threadIdx.x < RTW_MB_WORDS)  // the shared drain's mailbox (mb_slot): live = all waves
+            reinterpret_cast<uint32_t*>(smem + A.mb_off)[threadIdx.x] = threadIdx.x == 32 ? RTW_BLOCK / 64 : 0u;
         __syncthreads();
     }
     // the traversal stacks follow the LDS scene and the shading tables
@@ -2076,6 +2132,14 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     uint64_t wx_tref = 0, wx_tsah = 0, wx_tcoop = 0;
     bool wx_dry = false;
 #endif
+    // the shared drain (mb_slot): worlds whose drained rays coop_solve traces, LDS modes 1 and 2
+    // (its mailbox offset in a VGPR, read per use: a value live across the walk in an SGPR spills)
+    // (not plain-sphere worlds: final_scene1's drain is short, and the code cost it 0.8 %)
+    constexpr bool SHARE_K = !STATS && LDS_SCENE && LK <= LK_PLAIN && LK != LK_SPHERES;
+    int32_t mb_v = SHARE_K ? A.mb_off : -1;
+    asm volatile("" : "+v"(mb_v));
+    auto share_on = [&]() { return SHARE_K && __builtin_amdgcn_readfirstlane(mb_v) >= 0; };
+    auto mailbox = [&]() { return reinterpret_cast<uint32_t*>(smem + __builtin_amdgcn_readfirstlane(mb_v)); };
     for (;;) {
         if (__ballot(T.phase != PH_DONE) == 0) break;  // wave-uniform: every lane is done
         // 1. lanes without a pixel take the next items of the wave's reserve
@@ -2250,7 +2314,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
         // path (wave-uniform choice per call)
         if (sah) {
             // the drain: the walk stops when at most coop_max lanes still trace, and those rays (the
-            // long walks) are traced by the whole wave (coop_trace); wave-uniform condition
+            // long walks) are traced by the whole wave (coop_solve); wave-uniform condition
             const bool dry_coop = !STATS && LK <= LK_PLAIN && qfail >= RTW_QUEUES && A.coop_max > 0;
 #ifdef RTW_WAVE_TIMING
             uint64_t wx_t0 = wall_clock64();
@@ -2258,7 +2322,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, stabs, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
                                                        A.leaf_count, A.rect_count, A.tri_count, stack_off,
                                                        STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
-            // the rays coop_trace takes (one call site, inlined: as an out-of-line call taking and
+            // the rays coop_solve takes (one call site, inlined: as an out-of-line call taking and
             // returning Trav by value it cost 304 B of scratch per lane, saved and restored around
             // every call -- suzanne's and cornell_cube's extra write traffic): the drain's last rays
             unsigned long long coop = 0;
@@ -2272,12 +2336,78 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 #endif
                 if (tm != 0 && (uint32_t)__popcll(tm) <= (uint32_t)A.coop_max) coop = tm;
             }
-            // ... and the walk's tied rays: coop_trace finds every tied leaf and keeps the reference's
+            // ... and the walk's tied rays: coop_solve finds every tied leaf and keeps the reference's
             // (its DFS-first); a drained ray is traced once and leaves with its own ties resolved
             if (!STATS && LK <= LK_PLAIN && A.coop_ties)
                 coop |= __ballot(T.phase == PH_SHADE && (T.fast & (RTW_TF_SAH | RTW_TF_TIE)) == (RTW_TF_SAH | RTW_TF_TIE));
-            if (!STATS && LK <= LK_PLAIN && coop)
-                T = coop_trace<LDS, LK>(A.wdev, T, coop, A.node_count, A.leaf_count, A.rect_count, A.fast_off, A.coop_ties == 2);
+            // ... shared with the block's finished waves when no lane of this wave is inside a walk (the rays
+            // go to the stack columns): the mailbox, mb_slot
+            const bool own = share_on() && dry_coop && coop != 0 && (__ballot(T.phase == PH_TRACE) & ~coop) == 0;
+            const bool in = (coop >> lane) & 1;
+            const uint32_t post_j = (uint32_t)__popcll(coop & ((1ull << lane) - 1));  // the lane's ray, in order
+            const uint32_t post_k = own ? min((uint32_t)__popcll(coop), (uint32_t)A.mb_cap) : 0u;
+            if (own) {
+                uint32_t* mb = mailbox();
+                const int v = threadIdx.x >> 6;
+                if (in && post_j < post_k) {
+                    float4* q = mb_slot<LDS, LK>(stack_off, v, (int)post_j);
+                    q[0] = make_float4(T.ray.o.x, T.ray.o.y, T.ray.o.z, T.ray.time);
+                    q[1] = make_float4(T.ray.d.x, T.ray.d.y, T.ray.d.z, __int_as_float(T.fast));
+                    q[2] = make_float4(T.inv.x, T.inv.y, T.inv.z, 0.0f);
+                } else if (in && T.phase == PH_TRACE) {  // beyond the mailbox: the walk starts over (its stack is gone)
+                    T.node = LK == LK_SPHERES ? w.sah_root_c2 : w.sah_root;
+                    T.sp = 0;
+                    T.te = F32_INF;
+                    T.found = -1;
+                    T.fast &= ~RTW_TF_TIE;
+                }
+                if (lane == 0) {  // the batch's rays are written (release): open it
+                    const uint32_t s = __hip_atomic_load(&mb[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&mb[16 + v], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&mb[v], ((((s >> 16) + 1) & 0xFFFFu) << 16) | (post_k << 8), __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                coop = 0;
+            }
+            // the wave's own rays, one at a time (read from their lanes): `coop`, or this wave's posts that
+            // no helper has taken yet (a take as the helpers'); every answer of a post goes to its slot
+            if (!STATS && LK <= LK_PLAIN && (coop || own)) {
+                uint32_t* mb = mailbox();
+                const int v = threadIdx.x >> 6;
+                for (;;) {  // wave-uniform
+                    int src, j = 0;
+                    if (own) {
+                        if (!mb_take_own(mb, v, j)) break;
+                        src = __ffsll((long long)__ballot(in && post_j == (uint32_t)j)) - 1;
+                    } else {
+                        if (!coop) break;
+                        src = __ffsll((long long)coop) - 1;
+                        coop &= coop - 1;
+                    }
+                    CRay a;
+                    a.r.o = v3(__shfl(T.ray.o.x, src), __shfl(T.ray.o.y, src), __shfl(T.ray.o.z, src));
+                    a.r.d = v3(__shfl(T.ray.d.x, src), __shfl(T.ray.d.y, src), __shfl(T.ray.d.z, src));
+                    a.r.time = __shfl(T.ray.time, src);
+                    a.inv = v3(__shfl(T.inv.x, src), __shfl(T.inv.y, src), __shfl(T.inv.z, src));
+                    a.sgn = __shfl(T.fast, src);
+                    const CHit h = coop_solve<LDS, LK>(w, a, A.node_count, A.leaf_count, A.rect_count, A.fast_off,
+                                                       A.coop_ties == 2);
+                    if (!own) {
+                        if (lane == src) coop_apply(T, h.found, h.te, h.tie);
+                    } else if (lane == 0) {
+                        mb_answer(mb, mb_slot<LDS, LK>(stack_off, v, j), v, h);
+                    }
+                }
+                if (own) {  // the posts others took: wait for their answers, then every posted lane takes its own
+                    while ((uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
+                               &mb[16 + v], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < post_k)
+                        __builtin_amdgcn_s_sleep(1);
+                    if (in && post_j < post_k) {
+                        const float4 r = mb_slot<LDS, LK>(stack_off, v, (int)post_j)[3];
+                        coop_apply(T, __float_as_int(r.x), r.y, r.z != 0.0f);
+                    }
+                }
+            }
 #ifdef RTW_WAVE_TIMING
             const uint64_t wx_t1 = wall_clock64();
             if (qfail >= RTW_QUEUES) wx_tcoop += wx_t1 - wx_t0;
@@ -2423,6 +2553,33 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             } else {
                 fresh = true;  // the scattered ray continues the path
             }
+        }
+    }
+    // every lane is done: the wave traces the block's posted rays until no wave of the block is live (the
+    // poll bound only ends a helper early, never a ray: owners trace their own posts too)
+    if (share_on()) {
+        uint32_t* mb = mailbox();
+        if (lane == 0) __hip_atomic_fetch_add(&mb[32], ~0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (uint32_t polls = 0; polls < RTW_MB_POLLS; ++polls) {
+            int j = 0;
+            const int u = mb_take(mb, threadIdx.x >> 6, j);
+            if (u < 0) {
+                if (__builtin_amdgcn_readfirstlane(
+                        (int)__hip_atomic_load(&mb[32], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
+                    break;
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            float4* q = mb_slot<LDS, LK>(stack_off, u, j);
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+            CRay a;
+            a.r.o = v3(q0.x, q0.y, q0.z);
+            a.r.time = q0.w;
+            a.r.d = v3(q1.x, q1.y, q1.z);
+            a.sgn = __float_as_int(q1.w);
+            a.inv = v3(q2.x, q2.y, q2.z);
+            const CHit h = coop_solve<LDS, LK>(w, a, A.node_count, A.leaf_count, A.rect_count, A.fast_off, A.coop_ties == 2);
+            if (lane == 0) mb_answer(mb, q, u, h);
         }
     }
     RTW_PT_FLUSH;
@@ -3705,7 +3862,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const bool sah = (!stats || ktree) && g->sah_nodes > 0 && g->mk_world && lk <= LK_WRAPPED &&
                      g->sah_folded == (lk == LK_SPHERES);
     A.sah = sah ? 1 : 0;
-    // the drain's cooperative trace (coop_trace): worlds small enough to test every leaf per ray
+    // the drain's cooperative trace (coop_solve): worlds small enough to test every leaf per ray
     A.coop_max = g->leaf_count <= RTW_COOP_LEAVES ? (int32_t)env_size("RTW_COOP_MAX", RTW_COOP_MAX) : 0;
     if (const char* e = std::getenv("RTW_COOP_MAX"))
         if (e[0] == '0') A.coop_max = 0;
@@ -3773,6 +3930,21 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         A.sh_bx = A.sh_sph + g->sphere_count;
         A.stack_off += (int32_t)(gen_bytes / sizeof(float4));
         lds += gen_bytes;
+    }
+    // ... and the shared drain's mailbox after the stack (mb_slot; RTW_NO_COOP_SHARE=1: each wave drains
+    // alone).  A wave's stack columns hold depth x (entry bytes) rays of 64 B.
+    A.mb_off = -1;
+    A.mb_cap = 0;
+    const size_t stk_bytes = mode == 2 ? stack16_bytes : mode == 1 ? stack1_bytes : stack_bytes;
+    const int stk_entry = (mode == 2 || (mode == 1 && lk != LK_SPHERES)) ? 2 : 4;
+    const char* ncs = std::getenv("RTW_NO_COOP_SHARE");
+    if (!stats && mode >= 1 && sah && lk <= LK_PLAIN && lk != LK_SPHERES && A.coop_max > 0 && g->depth >= 1 &&
+        lds + RTW_MB_WORDS * sizeof(uint32_t) <= cap && !(ncs && ncs[0] && ncs[0] != '0')) {
+        A.mb_off = A.stack_off + (int32_t)(stk_bytes / sizeof(float4));
+        A.mb_cap = std::min(64, g->depth * stk_entry);
+        if (const char* e = std::getenv("RTW_MB_CAP"))  // tests: fewer posts per batch (the rest walk again)
+            A.mb_cap = std::max(1, std::min(A.mb_cap, std::atoi(e)));
+        lds += RTW_MB_WORDS * sizeof(uint32_t);
     }
     using KFn = void (*)(KArgs);
 #define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}

@@ -288,7 +288,7 @@ def test_coop_tie_resolution_decides_images(monkeypatch):
     out = torch.empty(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
     dw.render_into(R.render_params(R.Size2i(16, 16), 1, 50), out.data_ptr(), 0)
     torch.cuda.synchronize()
-    assert dw.kernel_variant()["leaf_kinds"] <= 2  # plain spheres / rects / triangles: coop_trace applies
+    assert dw.kernel_variant()["leaf_kinds"] <= 2  # plain spheres / rects / triangles: coop_solve applies
     size = R.Size2i(160, 90)
     gpu = R.render(size, 1, 8, 50, world, seed=41)
     assert_bit_identical(gpu, O.render(world, R.render_params(size, 8, 50, seed=41)), "tie world, coop ties")
@@ -300,6 +300,23 @@ def test_coop_tie_resolution_decides_images(monkeypatch):
     monkeypatch.setenv("RTW_COOP_AUDIT", "1")
     wrong = R.render(size, 1, 8, 50, world, seed=41)
     assert not np.array_equal(np.asarray(wrong), np.asarray(gpu)), "the DFS-last tied leaf gave the same image"
+
+
+@pytest.mark.parametrize("name", ["suzanne", "cornell_cube"])
+def test_shared_drain_bit_exact(worlds, name, monkeypatch):
+    """a wave's drained rays posted to the block's mailbox and traced by the block's
+    finished waves (or by the owner) give the image of each wave tracing its own (RTW_NO_COOP_SHARE=1);
+    with one or three posts per batch (RTW_MB_CAP) the rays beyond it walk again from the root, and
+    the image stays the same.  Most waves of a 240x135 x 16 frame drain."""
+    world = worlds(name)
+    size = R.Size2i(240, 135)
+    shared = R.render(size, 1, 16, 50, world, seed=19)
+    monkeypatch.setenv("RTW_NO_COOP_SHARE", "1")
+    assert_bit_identical(shared, R.render(size, 1, 16, 50, world, seed=19), f"{name}: shared vs private drain")
+    monkeypatch.delenv("RTW_NO_COOP_SHARE")
+    for cap in ("1", "3"):
+        monkeypatch.setenv("RTW_MB_CAP", cap)
+        assert_bit_identical(shared, R.render(size, 1, 16, 50, world, seed=19), f"{name}: {cap} posts per batch")
 
 
 def test_progress_callback_reports_and_keeps_bits(worlds):
