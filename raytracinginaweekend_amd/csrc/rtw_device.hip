@@ -477,8 +477,112 @@ __device__ __forceinline__ V3 d_unit_ball(rtw_xoro* r) {  // rtw_unit_ball
 
 // Out-of-line wrappers: the f64 polynomial constants need SGPR pairs (no VOP3 literals on
 // gfx9); inlined into the bounce loop they get hoisted and pin ~100 SGPRs.
-__device__ __noinline__ float d_acosf(float x) { return rtw_acosf(x); }
-__device__ __noinline__ float d_atan2f(float y, float x) { return rtw_atan2f(y, x); }
+// The sphere uv's acosf / atan2f (vec3.rs:242-243; rtw_scalar.h's restatements of glibc's fdlibm code,
+// the specification) with each IEEE division and square root replaced by div_x / sqrt_x: the same bits
+// (both exact, with the IEEE operation where their guards fail), the compiler's 11-instruction division
+// sequence and range-checked sqrt gone from every sphere-uv hit (earth_motion's shading).  Checked
+// against the host restatements by eval_scalar_kernel (tests/test_gpu_scalar.py).
+__device__ __forceinline__ float d_atanf_x(float x) {
+    const float atanhi[4] = {__uint_as_float(0x3eed6338u), __uint_as_float(0x3f490fdau), __uint_as_float(0x3f7b985eu),
+                             __uint_as_float(0x3fc90fdau)};
+    const float atanlo[4] = {__uint_as_float(0x31ac3769u), __uint_as_float(0x33222168u), __uint_as_float(0x33140fb4u),
+                             __uint_as_float(0x33a22168u)};
+    const float aT0 = __uint_as_float(0x3eaaaaabu), aT1 = __uint_as_float(0xbe4ccccdu), aT2 = __uint_as_float(0x3e124925u),
+                aT3 = __uint_as_float(0xbde38e38u), aT4 = __uint_as_float(0x3dba2e6eu), aT5 = __uint_as_float(0xbd9d8795u),
+                aT6 = __uint_as_float(0x3d886b35u), aT7 = __uint_as_float(0xbd6ef16bu), aT8 = __uint_as_float(0x3d4bda59u),
+                aT9 = __uint_as_float(0xbd15a221u), aT10 = __uint_as_float(0x3c8569d7u);
+    const int32_t hx = __float_as_int(x);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) {
+        if (ix < 0x31000000) return x;
+        id = -1;
+    } else {
+        x = __builtin_fabsf(x);
+        if (ix < 0x3f980000) {
+            if (ix < 0x3f300000) {
+                id = 0;
+                x = div_x(2.0f * x - 1.0f, 2.0f + x);
+            } else {
+                id = 1;
+                x = div_x(x - 1.0f, x + 1.0f);
+            }
+        } else if (ix < 0x401c0000) {
+            id = 2;
+            x = div_x(x - 1.5f, 1.0f + 1.5f * x);
+        } else {
+            id = 3;
+            x = div_x(-1.0f, x);
+        }
+    }
+    const float z = x * x;
+    const float w = z * z;
+    const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -r : r;
+}
+__device__ __noinline__ float d_acosf(float x) {
+    const float pi = __uint_as_float(0x40490fdau), pio2_hi = __uint_as_float(0x3fc90fdau), pio2_lo = __uint_as_float(0x33a22168u);
+    const float pS0 = __uint_as_float(0x3e2aaaabu), pS1 = __uint_as_float(0xbea6b090u), pS2 = __uint_as_float(0x3e4e0aa8u),
+                pS3 = __uint_as_float(0xbd241146u), pS4 = __uint_as_float(0x3a4f7f04u), pS5 = __uint_as_float(0x3811ef08u);
+    const float qS1 = __uint_as_float(0xc019d139u), qS2 = __uint_as_float(0x4001572du), qS3 = __uint_as_float(0xbf303361u),
+                qS4 = __uint_as_float(0x3d9dc62eu);
+    const int32_t hx = __float_as_int(x);
+    const int32_t ix = hx & 0x7fffffff;
+    if (ix == 0x3f800000) return hx > 0 ? 0.0f : pi + __uint_as_float(0x34222168u);
+    if (ix > 0x3f800000) return (x - x) / (x - x);
+    if (ix < 0x3f000000) {
+        if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+        const float z = x * x;
+        const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        return pio2_hi - (x - (pio2_lo - x * div_x(p, q)));
+    }
+    const float z = (hx < 0 ? 1.0f + x : 1.0f - x) * 0.5f;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float s = sqrt_x(z);
+    const float r = div_x(p, q);
+    if (hx < 0) return pi - 2.0f * (s + (r * s - pio2_lo));
+    const float df = __uint_as_float(__float_as_uint(s) & 0xfffff000u);
+    const float c = div_x(z - df * df, s + df);
+    return 2.0f * (df + (r * s + c));
+}
+__device__ __noinline__ float d_atan2f(float y, float x) {
+    const float tiny = __uint_as_float(0x0da24260u);
+    const float pi_o_4 = __uint_as_float(0x3f490fdbu), pi_o_2 = __uint_as_float(0x3fc90fdbu), pi = __uint_as_float(0x40490fdbu),
+                pi_lo = __uint_as_float(0xb3bbbd2eu);
+    const int32_t hx = __float_as_int(x), hy = __float_as_int(y);
+    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return d_atanf_x(y);
+    const int m = (int)(((uint32_t)hy >> 31) & 1u) | (int)(((uint32_t)hx >> 30) & 2u);
+    if (iy == 0) return m <= 1 ? y : m == 2 ? pi + tiny : -pi - tiny;
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000)
+            return m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny : m == 2 ? 3.0f * pi_o_4 + tiny : -3.0f * pi_o_4 - tiny;
+        return m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0f;
+    else z = d_atanf_x(__builtin_fabsf(div_x(y, x)));
+    switch (m) {
+        case 0: return z;
+        case 1: return __uint_as_float(__float_as_uint(z) ^ 0x80000000u);
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
 __device__ __noinline__ float d_logf(float x) { return rtw_logf(x); }
 __device__ __noinline__ float d_sinf(float x) { return rtw_sinf(x); }
 
@@ -2134,8 +2238,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 #endif
     // the shared drain (mb_slot): worlds whose drained rays coop_solve traces, LDS modes 1 and 2
     // (its mailbox offset in a VGPR, read per use: a value live across the walk in an SGPR spills)
-    // (not plain-sphere worlds: final_scene1's drain is short, and the code cost it 0.8 %)
-    constexpr bool SHARE_K = !STATS && LDS_SCENE && LK <= LK_PLAIN && LK != LK_SPHERES;
+    // Worlds of plain spheres and triangles only (leaf kinds 1: meshes that trap paths); elsewhere the
+    // code cost more than the drain gained (final_scene1 -0.8 %, cornell_cube -0.6 % with the same 8-way
+    // shares: profiles/r05/ab_shared_drain.txt, r5q_part8_coop.txt)
+    constexpr bool SHARE_K = !STATS && LDS_SCENE && LK == LK_TRIS;
     int32_t mb_v = SHARE_K ? A.mb_off : -1;
     asm volatile("" : "+v"(mb_v));
     auto share_on = [&]() { return SHARE_K && __builtin_amdgcn_readfirstlane(mb_v) >= 0; };
@@ -2789,8 +2895,8 @@ __global__ void eval_scalar_kernel(int fn, const float* a, const float* b, int64
     if (i >= n) return;
     float r;
     switch (fn) {
-        case 0: r = rtw_acosf(a[i]); break;
-        case 1: r = rtw_atan2f(a[i], b[i]); break;
+        case 0: r = d_acosf(a[i]); break;  // the render kernel's versions (div_x / sqrt_x inside)
+        case 1: r = d_atan2f(a[i], b[i]); break;
         case 2: r = rtw_logf(a[i]); break;
         case 3: r = rtw_sinf(a[i]); break;
         case 4: r = a[i] / b[i]; break;
@@ -3938,7 +4044,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const size_t stk_bytes = mode == 2 ? stack16_bytes : mode == 1 ? stack1_bytes : stack_bytes;
     const int stk_entry = (mode == 2 || (mode == 1 && lk != LK_SPHERES)) ? 2 : 4;
     const char* ncs = std::getenv("RTW_NO_COOP_SHARE");
-    if (!stats && mode >= 1 && sah && lk <= LK_PLAIN && lk != LK_SPHERES && A.coop_max > 0 && g->depth >= 1 &&
+    if (!stats && mode >= 1 && sah && lk == LK_TRIS && A.coop_max > 0 && g->depth >= 1 &&
         lds + RTW_MB_WORDS * sizeof(uint32_t) <= cap && !(ncs && ncs[0] && ncs[0] != '0')) {
         A.mb_off = A.stack_off + (int32_t)(stk_bytes / sizeof(float4));
         A.mb_cap = std::min(64, g->depth * stk_entry);

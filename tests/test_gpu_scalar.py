@@ -82,3 +82,27 @@ def test_checker_sign():
         want = ((s[:, 0] * s[:, 1]) * s[:, 2] < np.float32(0)).astype(np.int32)
     bad = np.nonzero(out != want)[0]
     assert len(bad) == 0, f"{len(bad)} mismatches, first {xyz[bad[:5]]}"
+
+
+def test_uv_functions_dense():
+    """The render kernel's acosf / atan2f (div_x / sqrt_x inside, rtw_device.hip d_acosf / d_atan2f)
+    against the host restatements: every f32 bit pattern in [-1, 1] of a 4M-value stride sample for
+    acos (all of its branches and their edges), and atan2 pairs whose ratios sit on both sides of
+    atanf's branch points (7/16, 11/16, 19/16, 39/16, 2^+-25) and of the 2^+-60 shortcuts."""
+    rng = np.random.default_rng(123)
+    bits = np.arange(0, 0x3F800001, 253, dtype=np.uint64).astype(np.uint32)
+    a = bits.view(np.float32)
+    a = np.concatenate([a, -a, np.float32([0.5, -0.5, 2.0**-26, -(2.0**-26), 2.0**-25])])
+    assert_bit_identical(_device(0, a), O.eval_scalar(0, a), "acos dense")
+    r = np.float32([7 / 16, 11 / 16, 19 / 16, 39 / 16, 2.0**25, 2.0**-29, 2.0**60, 2.0**-60, 1.0])
+    x = np.exp2(rng.uniform(-40, 40, 60_000)).astype(np.float32) * rng.choice([-1, 1], 60_000).astype(np.float32)
+    ys = []
+    xs = []
+    for q in r:
+        for d in (-2, -1, 0, 1, 2):
+            ratio = np.float32(q) * np.float32(1 + d * 2.0**-23)
+            ys.append((x * ratio).astype(np.float32) * rng.choice([-1, 1], len(x)).astype(np.float32))
+            xs.append(x)
+    y = np.concatenate(ys)
+    xx = np.concatenate(xs)
+    assert_bit_identical(_device(1, y, xx), O.eval_scalar(1, y, xx), "atan2 branch points")

@@ -70,6 +70,18 @@ def main():
           f"ends (ms) min {q[0]:.2f} p10 {q[1]:.2f} p50 {q[2]:.2f} p90 {q[3]:.2f} p99 {q[4]:.2f} max {q[5]:.2f}; "
           f"queue empty (ms) min {qd[0]:.2f} p50 {qd[1]:.2f} max {qd[2]:.2f}; drain after it p50 {dr[0]:.2f} p90 {dr[1]:.2f} "
           f"p99 {dr[2]:.2f} max {dr[3]:.2f}")
+    idx = np.nonzero(buf.reshape(-1, 3)[:, 1] > 0)[0]
+    blk = idx // 16  # RTW_BLOCK / 64 waves per block
+    ub, inv = np.unique(blk, return_inverse=True)
+    bend = np.full(len(ub), -1.0)
+    np.maximum.at(bend, inv, en)
+    bdry = np.full(len(ub), 1e30)
+    np.minimum.at(bdry, inv, dry)
+    qb = np.percentile(bend, [0, 10, 50, 90, 99, 100])
+    qbd = np.percentile(bend - bdry, [50, 90, 99, 100])
+    print(f"  blocks {len(ub)}: last wave ends (ms) min {qb[0]:.2f} p10 {qb[1]:.2f} p50 {qb[2]:.2f} p90 {qb[3]:.2f} "
+          f"p99 {qb[4]:.2f} max {qb[5]:.2f}; block drain (its last end - its first dry) p50 {qbd[0]:.2f} p90 {qbd[1]:.2f} "
+          f"p99 {qbd[2]:.2f} max {qbd[3]:.2f}")
     e = ext.reshape(-1, 8).astype(np.int64)[: len(buf) // 3]
     e = e[buf.reshape(-1, 3)[:, 1] > 0]
     order = np.argsort(-(en - dry))
