@@ -4164,7 +4164,7 @@ int grow(void** buf, size_t* have, size_t need) {
 
 // One frame: launches of at most RTW_SAMPLE_BUFFER_BYTES (default: half of the HBM this world could
 // use, at most 64 GiB) of per-sample colours,
-// each followed by the in-order accumulation; work items of RTW_CHUNK (default 8) samples.
+// each followed by the in-order accumulation; work items of RTW_CHUNK (default 1) samples.
 // Launch l of a frame takes its work items from queue block min(l, RTW_QUEUE_SLOTS - 1) of the
 // world's counters, so a progress poller can read how many items each launch has handed out.
 int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStream_t stream,

@@ -574,3 +574,38 @@ def test_suzanne_large_split_budget_bit_exact(worlds, monkeypatch):
     sah = R.render(big, 1, 8, 50, world, seed=29)
     monkeypatch.setenv("RTW_NO_SAH", "1")
     assert_bit_identical(sah, R.render(big, 1, 8, 50, world, seed=29), "suzanne split budget 4 vs reference tree")
+
+
+def _soup_world(n_tri: int, seed: int = 5):
+    """A random triangle soup over a ground sphere (mesh worlds of any size)."""
+    rng = np.random.default_rng(seed)
+    wb = R.WorldBuilder()
+    mats = [wb.material_lambert_solid((0.7, 0.3, 0.2)), wb.material_metal_solid((0.8, 0.8, 0.8), 0.2)]
+    g = wb.new_group()
+    g.add(wb.new_obj_sphere(100.0, mats[0]).translate((0.0, -100.0, 0.0)))
+    c = rng.uniform((-2.0, 0.2, -2.0), (2.0, 2.2, 2.0), (n_tri, 1, 3))
+    v = (c + rng.uniform(-0.25, 0.25, (n_tri, 3, 3))).astype(np.float32)
+    tris = np.concatenate([v.reshape(n_tri, 9), np.tile(np.float32([0, 1, 0]), (n_tri, 3)),
+                           np.zeros((n_tri, 6), np.float32)], 1).astype(np.float32)
+    g.add(wb.new_mesh(tris, mats[1]))
+    cam = R.Camera.build().vertical_fov(50.0, 9.0 / 16.0).position((0.0, 1.5, 6.0)).look_at((0, 1, 0), (0, 1, 0)).build()
+    return g.build().finish(wb, R.BackgroundColor.sky(), cam)
+
+
+@pytest.mark.parametrize("n_tri,mode2", [(300, True), (1100, False)])
+def test_triangle_records_lds_fallback(n_tri, mode2):
+    """LDS mode 2 holds the triangle records component-major with a fixed 1024-record stride
+    (RTW_TRI_SOA); a mesh world above it falls back to mode 1 (records from L2), which
+    rtw_world_kernel reports, and both render the oracle's bits."""
+    import torch
+
+    world = _soup_world(n_tri)
+    dw = R.DeviceWorld(world, 0)
+    out = torch.empty(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
+    dw.render_into(R.render_params(R.Size2i(16, 16), 1, 50), out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    v = dw.kernel_variant()
+    assert (v["lds_mode"] == 2) == mode2 and v["lds_mode"] >= 1, v
+    size = R.Size2i(40, 24)
+    assert_bit_identical(R.render(size, 1, 4, 50, world, seed=13), O.render(world, R.render_params(size, 4, 50, seed=13)),
+                         f"soup {n_tri}")

@@ -26,6 +26,8 @@ def main():
     g = c.get
     if g("SQ_ACTIVE_INST_VALU") and g("SQ_THREAD_CYCLES_VALU"):
         print(f"VALU lane utilisation        {g('SQ_THREAD_CYCLES_VALU') / (64 * g('SQ_ACTIVE_INST_VALU')):.3f}")
+    if g("SQ_LDS_BANK_CONFLICT") is not None and g("SQ_LDS_IDX_ACTIVE"):
+        print(f"LDS bank conflict / LDS-active cycles {g('SQ_LDS_BANK_CONFLICT') / g('SQ_LDS_IDX_ACTIVE'):.3f}")
     if g("SQ_WAVES") and g("SQ_INSTS_VALU"):
         print(f"VALU instr per wave          {g('SQ_INSTS_VALU') / g('SQ_WAVES'):.4e}")
     if g("SQ_WAIT_INST_ANY") and g("SQ_WAVE_CYCLES"):
