@@ -515,7 +515,7 @@ def main() -> int:
     roofline = {"bound": "valu_issue", "achieved": None, "peak": round(peak_ginstr, 1), "unit": "G VALU wave-instr/s",
                 "frac": None, "traffic": None,
                 "kernel": "render_kernel<false, LDS mode>; HIP events on its launch stream also span the in-order "
-                          "accumulate_kernel (~0.3 % of the frame)",
+                          "accumulate_kernel (~1.4 % of a 1080p x 512 frame: 1.95 ms, profiles/r05/r5z_kernel_stats.csv)",
                 "kernel_ms": round(kernel_ms, 3),
                 "peak_basis": f"{cus} CUs x {SIMDS_PER_CU} SIMD-32 x {CLOCK_GHZ} GHz / 2 cycles per wave64 VALU instruction"}
     if not args.no_stats:
