@@ -1328,20 +1328,25 @@ template <bool STATS, int TX, class TB>
 __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit& h, Stats& st,
                                              const TB& S) {  // texture.rs:23-53
     for (int guard = 0; guard < 64; ++guard) {
-        const int4 t0 = S.tex0 >= 0 ? lds_i4(S.tex0 + tex) : w.textures[3 * tex];
+        // the LDS table (launch_render, when it fits): solid-texture kernels each texture's first record,
+        // the other non-GEN kernels all three records, an image texture's third replaced by its image
+        // record (earth_mapped +3 %, perlin_spheres +5 %); the GEN kernels read HBM / L2 (as an LDS table
+        // it cost C5 1.3 % in spills, profiles/r05/ab_tex_lds.txt)
+        constexpr bool FULL = TX != TX_SOLID && !TB::gen;
+        const int4 t0 = S.tex0 >= 0 ? lds_i4(S.tex0 + (FULL ? 3 * tex : tex)) : w.textures[3 * tex];
         const int kind = t0.x;
         if (TX == TX_SOLID || kind == RTW_TEX_SOLID)
             return v3(__int_as_float(t0.y), __int_as_float(t0.z), __int_as_float(t0.w));
-        const int4 t1 = w.textures[3 * tex + 1];
+        const int4 t1 = FULL && S.tex0 >= 0 ? lds_i4(S.tex0 + 3 * tex + 1) : w.textures[3 * tex + 1];
         if (kind == RTW_TEX_CHECKER) {
             const float f = __int_as_float(t1.x);
             const V3 s = mul(h.pos, f);
             tex = d_checker_odd(s.x, s.y, s.z) ? t1.y : t1.z;  // sines < 0
             continue;
         }
-        const int4 t2 = w.textures[3 * tex + 2];
+        const int4 t2 = FULL && S.tex0 >= 0 ? lds_i4(S.tex0 + 3 * tex + 2) : w.textures[3 * tex + 2];
         if (kind == RTW_TEX_IMAGE) {
-            const int4 im = w.images[t2.y];
+            const int4 im = FULL && S.tex0 >= 0 ? t2 : w.images[t2.y];
             uint32_t pu = rtw_f2u32_sat(h.u * (float)im.y);
             uint32_t pv = rtw_f2u32_sat(h.v * (float)im.z);
             pu = min(pu, (uint32_t)(im.y - 1));
@@ -2143,7 +2148,15 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             }
             if (A.sh_tex0 >= 0) {
                 int4* tx = reinterpret_cast<int4*>(smem + A.sh_tex0);
-                for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
+                if constexpr (TX == TX_SOLID || GEN) {  // (the GEN kernels: -1, no table)
+                    for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
+                } else {  // all three records; an image texture's third is its image record
+                    for (int i = threadIdx.x; i < 3 * A.texture_count; i += RTW_BLOCK) {
+                        int4 r = w.textures[i];
+                        if (i % 3 == 2 && w.textures[i - 2].x == RTW_TEX_IMAGE) r = w.images[r.y];
+                        tx[i] = r;
+                    }
+                }
             }
         }
         if (A.mb_off >= 0 && threadIdx.x < RTW_MB_WORDS)  // the shared drain's mailbox (mb_slot): live = all waves
@@ -4006,12 +4019,17 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes + stack16_bytes : mode == 1 ? stack1_bytes : stack_bytes);
     // shading tables after the scene when they fit too (RTW_NO_SHADE_LDS=1: keep them in HBM / L2)
     const int32_t scene_f4 = (int32_t)((scene_bytes + (mode == 2 ? tri_bytes : 0)) / sizeof(float4));
-    const size_t sh_bytes = (size_t)(g->leaf_count + A.material_count + (tx == TX_SOLID ? A.texture_count : 0)) * sizeof(int4);
+    // the texture table (texture_sample): first records for solid-texture kernels, all three records for
+    // the other non-GEN kernels (the counting variants are TX_ANY, non-GEN), none for the GEN kernels
+    const char* ngl = std::getenv("RTW_NO_GEN_LDS");
+    const bool gen_wanted = !stats && lk >= LK_WRAPPED && !(ngl && ngl[0] && ngl[0] != '0');
+    const int tex_recs = (stats || tx != TX_SOLID) ? (gen_wanted ? 0 : 3) : 1;
+    const size_t sh_bytes = (size_t)(g->leaf_count + A.material_count + tex_recs * A.texture_count) * sizeof(int4);
     const char* nsl = std::getenv("RTW_NO_SHADE_LDS");
     const bool sh = mode >= 1 && lds + sh_bytes <= cap && !(nsl && nsl[0] && nsl[0] != '0');
     A.sh_li = sh ? scene_f4 : -1;
     A.sh_mat = sh ? scene_f4 + g->leaf_count : -1;
-    A.sh_tex0 = sh && tx == TX_SOLID ? scene_f4 + g->leaf_count + A.material_count : -1;
+    A.sh_tex0 = sh && tex_recs > 0 && A.texture_count > 0 ? scene_f4 + g->leaf_count + A.material_count : -1;
     A.stack_off = scene_f4 + (sh ? (int32_t)(sh_bytes / sizeof(int4)) : 0);
     if (sh) lds += sh_bytes;
     // ... and the SAH walk's proof boxes (one read per traced ray, else a dependent L2 read between the
@@ -4029,7 +4047,6 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     A.sh_xf = A.sh_sph = A.sh_bx = -1;
     A.sh_rect = mode >= 1 ? 2 * A.node_count + g->leaf_count + (sah && lk == LK_SPHERES ? 0 : (A.node_count + 1) / 2) : -1;
     const size_t gen_bytes = (size_t)(3 * g->leaf_count + g->sphere_count + 2 * g->box_count) * sizeof(float4);
-    const char* ngl = std::getenv("RTW_NO_GEN_LDS");
     if (sh && lk >= LK_WRAPPED && lds + gen_bytes <= cap && !(ngl && ngl[0] && ngl[0] != '0')) {
         A.sh_xf = A.stack_off;
         A.sh_sph = A.sh_xf + 3 * g->leaf_count;
