@@ -1,4 +1,5 @@
-# Audit builds (tools/build_variant.sh with -DRTW_SAH_AUDIT_NO_TIE / -DRTW_SAH_AUDIT_NO_BOX): the SAH walk's
+# Audit builds, made first (here, in-tree): RTW_VARIANT_FLAGS=-DRTW_SAH_AUDIT_NO_TIE bash tools/build_variant.sh notie,
+# and the same with -DRTW_SAH_AUDIT_NO_BOX as nobox (tools/build_variant.sh): the SAH walk's
 # tie test and leaf-box proof switched off.  The parity tests that exercise them must FAIL on these
 # libraries (a failure is the expected result: it shows that the switch decides pixels).  Run through
 # gpurun; output: gpurun_out/audit/.
