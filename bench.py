@@ -418,6 +418,7 @@ def main() -> int:
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=512)
+    ap.add_argument("--tile", default="8x8", help="partition tile WxH (the headline frame's; a wave takes one tile's pixels)")
     ap.add_argument("--max-depth", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -475,7 +476,8 @@ def main() -> int:
         return 0
 
     world = R.demo_world(args.scene)
-    spec = FrameSpec(R.Size2i(args.width, args.height), args.spp, args.max_depth, args.seed)
+    spec = FrameSpec(R.Size2i(args.width, args.height), args.spp, args.max_depth, args.seed,
+                     tile=tuple(int(x) for x in args.tile.lower().split("x")))
     fr = FrameRenderer(world, spec, rank, world_size, local_rank)
 
     for _ in range(args.warmup):
