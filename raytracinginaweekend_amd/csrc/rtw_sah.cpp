@@ -20,13 +20,18 @@ struct Item {
     int32_t id;  // leaf, encoded -1 - index
 };
 
-constexpr int kBins = 32;
+#ifndef RTW_OBJ_BINS
+// the object-split builder's bins: 128 against 32 gives final_scene1 16.55 node tests per random line
+// instead of 16.63 and +0.7 % on its frame (profiles/r05/ab_obj_bins.txt)
+#define RTW_OBJ_BINS 128
+#endif
+constexpr int kBins = RTW_OBJ_BINS;
 #ifndef RTW_SPLIT_BINS
 #define RTW_SPLIT_BINS 64
 #endif
 // the spatial-split builder's bins (object and spatial passes): 64 against 32 gives suzanne's budget-1
 // tree 1770 nodes instead of 1809 and 71.3 / 37.4 node / leaf tests per random line instead of 72.1 /
-// 37.6 (48, 80, 96, 128: between), +1.1 % on its frame (profiles/r05/ab_split_bins.txt)
+// 37.6 (48, 80, 96, 128: between), +0.9 % on its frame (profiles/r05/ab_split_bins.txt)
 constexpr int kSBins = RTW_SPLIT_BINS;
 constexpr int kSahDepth = 24;  // deeper subtrees split at the median (bounded stack)
 
