@@ -150,8 +150,18 @@ CONFIG_LEGS = (
 
 
 def _kernel_tag(v: dict) -> str:
-    """The render kernel's name fragment in rocprofv3's Kernel_Name for a kernel_variant() dict."""
-    return f"render_kernel<false, {v['lds_mode']}, {v['leaf_kinds']}, {v['tex_kinds']}>"
+    """The render kernel's name fragment in rocprofv3's Kernel_Name for a kernel_variant() dict: the
+    exact template name rtw_world_kernel_name reports (render_kernel<STATS, LDS, LK, TX, GEN>), rebuilt
+    from the fields for a dict without it (a GEN-less name then matches no row: configs_pmc says so)."""
+    if v.get("name"):
+        return v["name"]
+    return f"render_kernel<false, {v['lds_mode']}, {v['leaf_kinds']}, {v['tex_kinds']}, false>"
+
+
+def _match_rows(rows, tag: str) -> list:
+    """The rows of `rows` whose Kernel_Name holds the template name `tag` exactly (the counting variant's
+    render_kernel<true, ...> and other variants excluded)."""
+    return [x for x in rows or [] if tag in x["Kernel_Name"]]
 
 
 def render_configs(args, local_rank: int, steps: int, warmup: int, barrier) -> list:
@@ -211,11 +221,16 @@ def configs_pmc(args, legs: list, peak_ginstr: float) -> None:
         return
     a = _pmc_rows(child, list(VALU_COUNTERS) + ["WRITE_SIZE"])
     b = _pmc_rows(child, ["FETCH_SIZE"]) if a else None
+    names = sorted({x["Kernel_Name"] for x in (a or []) + (b or [])})
     for r, tag in zip(legs, tags):
-        v = _pmc_reduce([x for x in a or [] if tag in x["Kernel_Name"]])
-        f = _pmc_reduce([x for x in b or [] if tag in x["Kernel_Name"]])
+        v = _pmc_reduce(_match_rows(a, tag))
+        f = _pmc_reduce(_match_rows(b, tag))
         if not v or any(k not in v for k in VALU_COUNTERS) or not r.get("kernel_ms"):
+            # never a silent null: say which rows were looked for and what the passes saw
             r["roofline"] = None
+            r["pmc_note"] = (f"no PMC rows for {tag!r}" if a else "the VALU counter pass failed or rocprofv3 is "
+                             "absent") + (f"; render kernels in the passes: {names}" if names else "")
+            print(f"bench.py: configs leg {r['workload']}: {r['pmc_note']}", file=sys.stderr)
             continue
         k_s = r["kernel_ms"] * 1e-3
         achieved = v["SQ_INSTS_VALU"] / k_s / 1e9
@@ -516,8 +531,8 @@ def main() -> int:
     peak_ginstr = cus * SIMDS_PER_CU * CLOCK_GHZ / 2.0  # G wave-level VALU instructions / s
     roofline = {"bound": "valu_issue", "achieved": None, "peak": round(peak_ginstr, 1), "unit": "G VALU wave-instr/s",
                 "frac": None, "traffic": None,
-                "kernel": "render_kernel<false, LDS mode>; HIP events on its launch stream also span the in-order "
-                          "accumulate_kernel (~1.4 % of a 1080p x 512 frame: 1.95 ms, profiles/r05/r5z_kernel_stats.csv)",
+                "kernel": fr.dworld.kernel_variant().get("name") + "; HIP events on its launch stream also span the "
+                          "in-order accumulate_kernel (~1.4 % of a 1080p x 512 frame: 1.95 ms, profiles/r05/r5z_kernel_stats.csv)",
                 "kernel_ms": round(kernel_ms, 3),
                 "peak_basis": f"{cus} CUs x {SIMDS_PER_CU} SIMD-32 x {CLOCK_GHZ} GHz / 2 cycles per wave64 VALU instruction"}
     if not args.no_stats:

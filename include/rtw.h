@@ -272,6 +272,10 @@ typedef struct rtw_multi rtw_multi;
 RTW_API int rtw_multi_create(const rtw_world* world, const int* devices, int n_devices, rtw_multi** out);
 RTW_API int rtw_multi_render(rtw_multi* m, const rtw_render_params* params, float* d_image);
 RTW_API int rtw_multi_release(rtw_multi* m);
+/* Tile-buffer copies this rtw_multi made with hipMemcpyPeerAsync (partitions on a device other than
+ * devices[0]; with RTW_MULTI_FORCE_PEER=1 in the environment at rtw_multi_create, every partition's:
+ * a same-device peer copy, so one GPU runs the path distinct devices take).  Diagnostics only. */
+RTW_API int rtw_multi_peer_copies(const rtw_multi* m, uint64_t* copies);
 
 /* Resident path: upload once, render many times into device memory. */
 RTW_API int rtw_world_upload(const rtw_world* world, int device, rtw_gpu_world** out);
@@ -286,6 +290,11 @@ RTW_API int rtw_world_tuning(rtw_gpu_world* gw, int* trace_min);
  * the reference-order proof and fallback); -1 each before the first render.
  * Diagnostics only. */
 RTW_API int rtw_world_kernel(rtw_gpu_world* gw, int* lds_mode, int* leaf_kinds, int* tex_kinds, int* tree);
+/* The exact template name of that kernel, as profilers print it inside the demangled symbol
+ * ("render_kernel<false, 1, 0, 0, false>": counting variant, LDS mode, leaf kinds, texture kinds,
+ * generic leaf tables in LDS), NUL-terminated into buf[0..cap); "" before the first render.
+ * RTW_ERR_INVALID_ARGUMENT if cap is too small.  Diagnostics only (bench.py matches PMC rows by it). */
+RTW_API int rtw_world_kernel_name(rtw_gpu_world* gw, char* buf, int cap);
 /* The shape of this world's last frame (rtw_render_device / rtw_render on it): render-kernel launches,
  * whether the work items were whole pixels (1: samples summed in registers, no colour buffer, DESIGN.md
  * 5.5b; 0: single samples through the colour buffer), and the dynamic-fetch threshold it ran with (the

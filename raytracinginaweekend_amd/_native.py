@@ -243,6 +243,7 @@ _SIGS = {
     "rtw_world_release": (C.c_int, [_P]),
     "rtw_world_tuning": (C.c_int, [_P, C.POINTER(C.c_int)]),
     "rtw_world_kernel": (C.c_int, [_P] + [C.POINTER(C.c_int)] * 4),
+    "rtw_world_kernel_name": (C.c_int, [_P, C.c_char_p, C.c_int]),
     "rtw_world_last_frame": (C.c_int, [_P] + [C.POINTER(C.c_int)] * 3),
     "rtw_render_device": (C.c_int, [_P, C.POINTER(RenderParams), _P, _P]),
     "rtw_render_devices": (C.c_int, [C.POINTER(World), C.POINTER(RenderParams), C.POINTER(C.c_int), C.c_int,
@@ -250,6 +251,7 @@ _SIGS = {
     "rtw_multi_create": (C.c_int, [C.POINTER(World), C.POINTER(C.c_int), C.c_int, C.POINTER(_P)]),
     "rtw_multi_render": (C.c_int, [_P, C.POINTER(RenderParams), _P]),
     "rtw_multi_release": (C.c_int, [_P]),
+    "rtw_multi_peer_copies": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "rtw_partition_floats": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int64)]),
     "rtw_untile_device": (C.c_int, [C.POINTER(RenderParams), _P, C.c_int64, _P, _P]),
     "rtw_render_collect_stats": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(RenderStats)]),

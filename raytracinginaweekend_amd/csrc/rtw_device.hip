@@ -1602,6 +1602,10 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
     return o;
 }
 
+// the block-shared drain's traffic (rtw_debug_drain_counts; tests): rays posted to a mailbox, posts traced
+// by another wave of the block, posts traced by their owner (one atomic per batch or ray, drain only)
+__device__ unsigned long long rtw_drain_counts[3];
+
 #ifdef RTW_WAVE_TIMING  // experiment builds: per-wave start / end / queue-empty wall clocks of the last launch
 __device__ unsigned long long rtw_wave_times[3 * 8192];
 __device__ unsigned long long rtw_wave_dry[8192];  // first time a lane of the wave found the queue empty
@@ -1654,6 +1658,14 @@ struct Trav {
 // the RNG update alone made the compiler copy the lane's traversal registers at the leaf merge on
 // every leaf step.
 enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_WRAPPED = 3, LK_ANY = 4 };
+// Bytes per traversal-stack entry of render_kernel<.., LDS, LK, ..> -- the one predicate traverse's
+// StackEntry, the shared drain's mailbox slots (mb_slot) and launch_render's LDS sizing all use: 16-bit
+// node / leaf indices in LDS modes 1 and 2 (worlds below 2^15 nodes and leaves, checked at launch), 32-bit
+// where the scene is in HBM and in the plain-sphere worlds' mode 1, whose two-children walk pushes packed
+// children words (sah_left / sah_right).
+__host__ __device__ constexpr int stack_entry_bytes(int lds, int lk) {
+    return (lds == 2 || (lds == 1 && lk != LK_SPHERES)) ? 2 : 4;
+}
 template <bool STATS, int LDS, int LK, bool FAST_ONLY, int TM, class TB>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB& S, Trav T, int32_t trace_min,
                                       int32_t n_nodes, int32_t n_leaves, int32_t n_rects, int32_t n_tris,
@@ -1686,7 +1698,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB
     // 16-bit entries in the LDS modes (launch_render takes them only for worlds of < 2^15 nodes and
     // leaves): half the stack bytes, room for a deeper SAH tree or the triangle records -- except in
     // plain-sphere worlds, whose two-children walk pushes packed children words
-    using StackEntry = std::conditional_t<(LDS == 2 || (LDS == 1 && LK != LK_SPHERES)), int16_t, int32_t>;
+    using StackEntry = std::conditional_t<stack_entry_bytes(LDS, LK) == 2, int16_t, int32_t>;
     StackEntry* stack = reinterpret_cast<StackEntry*>(smem + stack_off) + threadIdx.x;
     // a leaf's root t: the reference narrows te to it; the SAH walk keeps te = succ(closest t) so
     // that a leaf reporting exactly the closest t again (a tie, whose winner is the reference's
@@ -2053,7 +2065,7 @@ __device__ __forceinline__ void coop_apply(Trav& T, int32_t found, float te, boo
 template <int LDS, int LK>
 __device__ __forceinline__ float4* mb_slot(int32_t stack_off, int v, int j) {
     // the stack's entry size (traverse's StackEntry): a wave's 64 entries of one level hold ES rays
-    constexpr int ES = (LDS == 2 || (LDS == 1 && LK != LK_SPHERES)) ? 2 : 4;
+    constexpr int ES = stack_entry_bytes(LDS, LK);
     return smem + stack_off + (j / ES) * (RTW_BLOCK * ES / 16) + v * (64 * ES / 16) + (j % ES) * 4;
 }
 // the owner's take of its own next post (wave-uniform); false: all taken
@@ -2481,6 +2493,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     T.fast &= ~RTW_TF_TIE;
                 }
                 if (lane == 0) {  // the batch's rays are written (release): open it
+                    atomicAdd(&rtw_drain_counts[0], (unsigned long long)post_k);
                     const uint32_t s = __hip_atomic_load(&mb[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(&mb[16 + v], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(&mb[v], ((((s >> 16) + 1) & 0xFFFFu) << 16) | (post_k << 8), __ATOMIC_RELEASE,
@@ -2515,6 +2528,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         if (lane == src) coop_apply(T, h.found, h.te, h.tie);
                     } else if (lane == 0) {
                         mb_answer(mb, mb_slot<LDS, LK>(stack_off, v, j), v, h);
+                        atomicAdd(&rtw_drain_counts[2], 1ull);
                     }
                 }
                 if (own) {  // the posts others took: wait for their answers, then every posted lane takes its own
@@ -2698,7 +2712,10 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             a.sgn = __float_as_int(q1.w);
             a.inv = v3(q2.x, q2.y, q2.z);
             const CHit h = coop_solve<LDS, LK>(w, a, A.node_count, A.leaf_count, A.rect_count, A.fast_off, A.coop_ties == 2);
-            if (lane == 0) mb_answer(mb, q, u, h);
+            if (lane == 0) {
+                mb_answer(mb, q, u, h);
+                atomicAdd(&rtw_drain_counts[1], 1ull);
+            }
         }
     }
     RTW_PT_FLUSH;
@@ -3324,14 +3341,15 @@ SahTables build_sah_tables(const rtw_world* w) {
         for (rtw_bvh_node& n : nodes)
             if (n.left >= 0 && n.right < 0) std::swap(n.left, n.right);
     // plain-sphere worlds (the two-children walk): node records sah_left / sah_right with m, children
-    // 15-bit signed (at most 2^14 - 1 nodes and 2^14 leaves, else the reference tree), k per world
-    // (DWorld::sah_k), the root's children word as the walk's first lane state; other worlds: node_b as
-    // the reference tree's and the cull constants in sah_km
+    // 15-bit signed (at most 2^14 - 1 nodes and 2^14 leaves), k per world (DWorld::sah_k), the root's
+    // children word as the walk's first lane state; other worlds -- and plain-sphere worlds above those
+    // limits, which then take the one-child walk of the triangle loop (rtw_world_upload) rather than
+    // losing the SAH tree -- node_b as the reference tree's and the cull constants in sah_km
     bool plain_spheres = true;
     for (int32_t i = 0; i < L; ++i)
         if (w->leaves[i].geom_kind != RTW_GEOM_SPHERE || w->leaves[i].flags != 0) plain_spheres = false;
+    if (plain_spheres && (nodes.size() >= 16384 || L > 16384)) plain_spheres = false;
     S.folded = plain_spheres;
-    if (plain_spheres && (nodes.size() >= 16384 || L > 16384)) return S;
     auto kids = [](const rtw_bvh_node& n) {
         return (int32_t)((uint32_t)n.axis | (((uint32_t)n.left & 0x7FFFu) << 2) | ((uint32_t)n.right << 17));
     };
@@ -3426,7 +3444,8 @@ struct rtw_gpu_world {
     bool done_recorded = false;
     uint32_t order_tiles = 0;
     bool order_valid = false;      // tile permutation computed for order_key
-    int32_t last_kernel[4] = {-1, -1, -1, -1};  // LDS mode, leaf kinds, texture kinds, tree of the last render
+    // LDS mode, leaf kinds, texture kinds, tree, GEN (generic leaf tables in LDS) of the last render
+    int32_t last_kernel[5] = {-1, -1, -1, -1, -1};
     // the last frame: render launches, whole-pixel items, the default threshold, in-frame tuning on
     int32_t last_frame[4] = {-1, -1, -1, 0};
 };
@@ -3456,6 +3475,20 @@ extern "C" RTW_API int rtw_debug_wave_extra(unsigned long long* out65536) {
     (void)out65536;
     return rtw::fail(RTW_ERR_UNSUPPORTED, "built without RTW_WAVE_TIMING");
 #endif
+}
+
+// tests: the block-shared drain's counters (rtw_drain_counts: rays posted, traced by helper waves, traced by
+// their owners) summed over the device's launches since the last reset; reset != 0 zeroes them after reading
+extern "C" RTW_API int rtw_debug_drain_counts(int device, unsigned long long* out3, int reset) {
+    if (!out3) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out3, HIP_SYMBOL(rtw_drain_counts), 3 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[3] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rtw_drain_counts), z, sizeof(z)));
+    }
+    return RTW_OK;
 }
 
 // experiment builds (-DRTW_PHASE_TIMING): read and reset the phase cycle sums
@@ -3722,6 +3755,9 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
                                                                         : LK_SPHERES;
         g->leaf_kinds = std::max(g->leaf_kinds, (int32_t)need);
     }
+    // a plain-sphere world beyond the folded records' 2^14 nodes / leaves keeps an unfolded SAH tree: the
+    // triangle loop (which tests plain spheres too) walks it with the one-child walk
+    if (g->leaf_kinds == LK_SPHERES && g->sah_nodes > 0 && !g->sah_folded) g->leaf_kinds = LK_TRIS;
     for (int i = 0; i < w->node_count; ++i)
         for (int k = 0; k < 3; ++k)
             for (float c : {w->nodes[i].min[k], w->nodes[i].max[k]})
@@ -3875,6 +3911,17 @@ extern "C" RTW_API int rtw_world_kernel(rtw_gpu_world* g, int* lds_mode, int* le
     return RTW_OK;
 }
 
+extern "C" RTW_API int rtw_world_kernel_name(rtw_gpu_world* g, char* buf, int cap) {
+    if (!g || !buf || cap < 1) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    char s[64] = "";
+    if (g->last_kernel[0] >= 0)  // the product kernel: render_kernel<STATS = false, LDS, LK, TX, GEN>
+        std::snprintf(s, sizeof(s), "render_kernel<false, %d, %d, %d, %s>", g->last_kernel[0], g->last_kernel[1],
+                      g->last_kernel[2], g->last_kernel[4] ? "true" : "false");
+    if ((int)std::strlen(s) >= cap) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "buffer too small");
+    std::memcpy(buf, s, std::strlen(s) + 1);
+    return RTW_OK;
+}
+
 extern "C" RTW_API int rtw_world_last_frame(rtw_gpu_world* g, int* launches, int* whole_pixel, int* trace_min) {
     if (!g || !launches || !whole_pixel || !trace_min) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
     *launches = g->last_frame[0];
@@ -3999,7 +4046,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
 #endif
     const size_t tri_bytes = (size_t)4 * RTW_TRI_SOA * sizeof(float4);  // mode 2: component-major, fixed stride
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
-    const size_t stack16_bytes = stack_bytes / 2;  // mode 2: 16-bit entries
+    const size_t stack16_bytes = stack_bytes / 2;  // 16-bit entries
     const char* lds_mode_env = std::getenv("RTW_LDS_MODE");  // audits: cap the mode
     A.node_count = sah ? g->sah_nodes : g->node_count;
     // LDS scene: [node_a n][node_b n][leaf records L][cull constants (n + 1) / 2, reference tree only][rects
@@ -4011,10 +4058,13 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     int mode = 0;
     // 16-bit stack entries (traverse's StackEntry): worlds of < 2^15 nodes (both trees) and leaves
     const bool small = g->leaf_count < 32768 && A.node_count < 32768 && g->node_count < 32768;
-    const size_t stack1_bytes = lk != LK_SPHERES ? stack16_bytes : stack_bytes;  // mode 1
+    // the LK template argument of the kernel launch_render picks below (the counting variant of a world
+    // without the SAH walk runs the LK_ANY loop): its stack entries are the ones the LDS must hold
+    const int kernel_lk = stats && !sah ? (int)LK_ANY : lk;
+    const size_t stack1_bytes = (size_t)stack_entry_bytes(1, kernel_lk) * g->depth * RTW_BLOCK;  // mode 1
     if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && small && scene_bytes + tri_bytes + stack16_bytes <= cap)
         mode = 2;
-    else if (scene_bytes + stack1_bytes <= cap && (small || lk == LK_SPHERES)) mode = 1;
+    else if (scene_bytes + stack1_bytes <= cap && (small || stack_entry_bytes(1, kernel_lk) == 4)) mode = 1;
     if (lds_mode_env) mode = std::min(mode, std::atoi(lds_mode_env));
     size_t lds = (mode >= 1 ? scene_bytes : 0) + (mode == 2 ? tri_bytes + stack16_bytes : mode == 1 ? stack1_bytes : stack_bytes);
     // shading tables after the scene when they fit too (RTW_NO_SHADE_LDS=1: keep them in HBM / L2)
@@ -4059,7 +4109,10 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     A.mb_off = -1;
     A.mb_cap = 0;
     const size_t stk_bytes = mode == 2 ? stack16_bytes : mode == 1 ? stack1_bytes : stack_bytes;
-    const int stk_entry = (mode == 2 || (mode == 1 && lk != LK_SPHERES)) ? 2 : 4;
+    const int stk_entry = stack_entry_bytes(mode, kernel_lk);
+    // the allocation holds the kernel's entries, and 16-bit entries hold every node and leaf index
+    if ((size_t)stk_entry * g->depth * RTW_BLOCK != stk_bytes || (stk_entry == 2 && !small))
+        return rtw::fail(RTW_ERR_UNSUPPORTED, "traversal stack entry width does not match the LDS allocation");
     const char* ncs = std::getenv("RTW_NO_COOP_SHARE");
     if (!stats && mode >= 1 && sah && lk == LK_TRIS && A.coop_max > 0 && g->depth >= 1 &&
         lds + RTW_MB_WORDS * sizeof(uint32_t) <= cap && !(ncs && ncs[0] && ncs[0] != '0')) {
@@ -4098,6 +4151,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         g->last_kernel[1] = lk;
         g->last_kernel[2] = tx;
         g->last_kernel[3] = sah ? 1 : 0;
+        g->last_kernel[4] = gen ? 1 : 0;
     }
     const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

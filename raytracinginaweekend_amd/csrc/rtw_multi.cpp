@@ -12,6 +12,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <string>
 #include <thread>
 #include <vector>
@@ -28,6 +30,10 @@ struct rtw_multi {
     size_t gather_floats = 0;
     float* image = nullptr;            // W x H x 3 on devices[0] (rtw_render_devices' own frame)
     size_t image_floats = 0;
+    // RTW_MULTI_FORCE_PEER=1 at create: partitions on devices[0] too copy with hipMemcpyPeerAsync (a
+    // same-device peer copy), so the one-GPU box runs the copy distinct devices take
+    bool force_peer = false;
+    std::atomic<uint64_t> peer_copies{0};  // hipMemcpyPeerAsync calls so far (rtw_multi_peer_copies)
 };
 
 namespace {
@@ -92,6 +98,7 @@ extern "C" RTW_API int rtw_multi_create(const rtw_world* world, const int* devic
     for (int i = 0; i < n_devices; ++i)
         if (devices[i] < 0 || devices[i] >= ndev) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "device index out of range");
     auto* m = new rtw_multi;
+    if (const char* e = std::getenv("RTW_MULTI_FORCE_PEER")) m->force_peer = e[0] == '1';
     m->devices.assign(devices, devices + n_devices);
     m->worlds.assign((size_t)n_devices, nullptr);
     m->streams.assign((size_t)n_devices, nullptr);
@@ -165,9 +172,11 @@ extern "C" RTW_API int rtw_multi_render(rtw_multi* m, const rtw_render_params* p
         if (rc != RTW_OK) return failed(rc, rtw_last_error());
         float* dst = m->gather + (size_t)i * (size_t)stride;
         const size_t bytes = (size_t)floats * sizeof(float);
+        const bool peer = d != d0 || m->force_peer;
         hipError_t e = bytes == 0 ? hipSuccess
-                       : d == d0  ? hipMemcpyAsync(dst, m->tiles[(size_t)i], bytes, hipMemcpyDeviceToDevice, s)
+                       : !peer    ? hipMemcpyAsync(dst, m->tiles[(size_t)i], bytes, hipMemcpyDeviceToDevice, s)
                                   : hipMemcpyPeerAsync(dst, d0, m->tiles[(size_t)i], d, bytes, s);
+        if (bytes != 0 && peer && e == hipSuccess) m->peer_copies.fetch_add(1, std::memory_order_relaxed);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return failed(RTW_ERR_HIP, std::string("partition copy: ") + hipGetErrorString(e));
     };
@@ -188,6 +197,12 @@ extern "C" RTW_API int rtw_multi_render(rtw_multi* m, const rtw_render_params* p
     const int rc = rtw_untile_device(&q, m->gather, stride, d_image, (void*)m->streams[0]);
     if (rc != RTW_OK) return rc;
     MT_TRY(hipStreamSynchronize(m->streams[0]));
+    return RTW_OK;
+}
+
+extern "C" RTW_API int rtw_multi_peer_copies(const rtw_multi* m, uint64_t* copies) {
+    if (!m || !copies) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
+    *copies = m->peer_copies.load(std::memory_order_relaxed);
     return RTW_OK;
 }
 

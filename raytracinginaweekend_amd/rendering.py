@@ -133,6 +133,12 @@ class MultiDeviceWorld:
         """One frame into the W*H*3 f32 device buffer at d_image_ptr (on devices[0])."""
         check(lib().rtw_multi_render(self._h, C.byref(params), C.c_void_p(d_image_ptr)))
 
+    def peer_copies(self) -> int:
+        """Tile-buffer copies made with hipMemcpyPeerAsync so far (rtw_multi_peer_copies)."""
+        v = C.c_uint64()
+        check(lib().rtw_multi_peer_copies(self._h, C.byref(v)))
+        return v.value
+
     def release(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().rtw_multi_release(self._h)
@@ -177,11 +183,16 @@ class DeviceWorld:
         return v.value
 
     def kernel_variant(self) -> dict:
-        """The render-kernel variant of the last render (LDS mode, leaf kinds, texture kinds, tree)."""
+        """The render-kernel variant of the last render (LDS mode, leaf kinds, texture kinds, tree, and the
+        kernel's exact template name)."""
         m, lk, tx, tr = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         check(lib().rtw_world_kernel(self._h, C.byref(m), C.byref(lk), C.byref(tx), C.byref(tr)))
+        name = C.create_string_buffer(64)
+        check(lib().rtw_world_kernel_name(self._h, name, 64))
         return {"lds_mode": m.value, "leaf_kinds": lk.value, "tex_kinds": tx.value,
-                "tree": ("reference", "sah")[tr.value] if tr.value >= 0 else None}
+                "tree": ("reference", "sah")[tr.value] if tr.value >= 0 else None,
+                # the exact template name (GEN included), as rocprofv3's Kernel_Name holds it
+                "name": name.value.decode()}
 
     def last_frame(self) -> dict:
         """The shape of the last frame: render launches, whole-pixel work items (no colour buffer),

@@ -42,4 +42,42 @@ def test_config_legs_are_the_baseline_configs():
     assert legs == {("suzanne", 1920, 1080, 512), ("cornell_cube", 800, 800, 1024), ("earth_motion", 3840, 2160, 2048)}
     for (n, w, h, spp, label), cfg in zip(bench.CONFIG_LEGS, (base["configs"][3], base["configs"][2], base["configs"][4])):
         assert f"{w}×{h}" in cfg and f"{spp}spp" in cfg, (label, cfg)
-    assert bench._kernel_tag({"lds_mode": 2, "leaf_kinds": 1, "tex_kinds": 0}) == "render_kernel<false, 2, 1, 0>"
+    assert bench._kernel_tag({"lds_mode": 2, "leaf_kinds": 1, "tex_kinds": 0}) == "render_kernel<false, 2, 1, 0, false>"
+
+
+def test_kernel_tag_matches_recorded_rocprof_names():
+    """Round 5's configs rooflines were null because the tag lacked the GEN template argument: the tag
+    from rtw_world_kernel_name must select exactly the product kernel's rows of a recorded rocprofv3
+    summary (profiles/r05/r7i_kernel_stats.csv), not the counting variant's."""
+    import csv
+
+    path = os.path.join(os.path.dirname(bench.__file__), "profiles", "r05", "r7i_kernel_stats.csv")
+    rows = [{"Kernel_Name": r["Name"]} for r in csv.DictReader(open(path))]
+    tag = bench._kernel_tag({"lds_mode": 1, "leaf_kinds": 0, "tex_kinds": 0, "name": "render_kernel<false, 1, 0, 0, false>"})
+    got = bench._match_rows(rows, tag)
+    assert len(got) == 1 and "render_kernel<false, 1, 0, 0, false>((anonymous namespace)::KArgs)" in got[0]["Kernel_Name"]
+    # the round-5 tag (no GEN argument) matched nothing
+    assert bench._match_rows(rows, "render_kernel<false, 1, 0, 0>") == []
+    # a GEN kernel's name differs from its non-GEN sibling's
+    gen = bench._kernel_tag({"lds_mode": 1, "leaf_kinds": 3, "tex_kinds": 1, "name": "render_kernel<false, 1, 3, 1, true>"})
+    assert bench._match_rows([{"Kernel_Name": "void (anonymous namespace)::render_kernel<false, 1, 3, 1, false>(KArgs)"}], gen) == []
+
+
+def test_configs_pmc_notes_unmatched_rows(monkeypatch):
+    """A config whose kernel has no PMC rows gets roofline None *and* a pmc_note naming what was seen."""
+    rows = [{"Kernel_Name": "void render_kernel<false, 1, 1, 0, false>(KArgs)", "Dispatch_Id": "1",
+             "Counter_Name": c, "Counter_Value": "1", "Start_Timestamp": "0", "End_Timestamp": "1"}
+            for c in bench.VALU_COUNTERS + ("WRITE_SIZE", "FETCH_SIZE")]
+    monkeypatch.setattr(bench, "_pmc_rows", lambda child, counters: rows)
+
+    class A:
+        max_depth, seed = 50, 1
+
+    legs = [{"workload": "suzanne", "kernel": {"name": "render_kernel<false, 1, 1, 0, false>"}, "kernel_ms": 1.0,
+             "colour_record_bytes": 12},
+            {"workload": "earth_motion", "kernel": {"name": "render_kernel<false, 1, 3, 1, true>"}, "kernel_ms": 1.0,
+             "colour_record_bytes": 12}]
+    bench.configs_pmc(A, legs, 1228.8)
+    assert legs[0]["roofline"] is not None and legs[0]["roofline"]["traffic"] is not None
+    assert "lane_utilisation" in legs[0]["roofline"] and "pmc_note" not in legs[0]
+    assert legs[1]["roofline"] is None and "render_kernel<false, 1, 3, 1, true>" in legs[1]["pmc_note"]

@@ -302,21 +302,55 @@ def test_coop_tie_resolution_decides_images(monkeypatch):
     assert not np.array_equal(np.asarray(wrong), np.asarray(gpu)), "the DFS-last tied leaf gave the same image"
 
 
-@pytest.mark.parametrize("name", ["suzanne", "cornell_cube"])
+def _drain_counts(reset: bool = True) -> tuple:
+    """(rays posted, posts traced by helper waves, posts traced by their owner) since the last reset
+    (rtw_debug_drain_counts: the block-shared drain's counters in the product kernel)."""
+    import ctypes as C
+
+    from raytracinginaweekend_amd import _native as N
+
+    fn = N.lib().rtw_debug_drain_counts
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_int, C.POINTER(C.c_uint64), C.c_int]
+    out = (C.c_uint64 * 3)()
+    N.check(fn(0, out, 1 if reset else 0))
+    return tuple(int(x) for x in out)
+
+
+@pytest.mark.parametrize("name", ["suzanne", "soup"])
 def test_shared_drain_bit_exact(worlds, name, monkeypatch):
     """a wave's drained rays posted to the block's mailbox and traced by the block's
     finished waves (or by the owner) give the image of each wave tracing its own (RTW_NO_COOP_SHARE=1);
     with one or three posts per batch (RTW_MB_CAP) the rays beyond it walk again from the root, and
-    the image stays the same.  Most waves of a 240x135 x 16 frame drain."""
-    world = worlds(name)
+    the image stays the same.  Both worlds take the shared drain (leaf kinds 1: plain spheres and
+    triangles; suzanne in LDS mode 1, the soup in mode 2), and the drain's counters show that rays were
+    posted and that other waves traced some of them (the test must not pass vacuously)."""
+    import torch
+
+    world = worlds(name) if name != "soup" else _soup_world(300)
+    dw = R.DeviceWorld(world, 0)
+    out = torch.empty(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
+    dw.render_into(R.render_params(R.Size2i(16, 16), 1, 50), out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    v = dw.kernel_variant()
+    assert v["leaf_kinds"] == 1 and v["tree"] == "sah" and v["lds_mode"] >= 1, v
+    dw.release()
     size = R.Size2i(240, 135)
+    _drain_counts()
     shared = R.render(size, 1, 16, 50, world, seed=19)
+    posted, helped, owned = _drain_counts()
+    assert posted > 0 and posted == helped + owned, (posted, helped, owned)
+    if name == "suzanne":  # trapped paths: blocks drain long after their first waves finish
+        assert helped > 0, (posted, helped, owned)
     monkeypatch.setenv("RTW_NO_COOP_SHARE", "1")
     assert_bit_identical(shared, R.render(size, 1, 16, 50, world, seed=19), f"{name}: shared vs private drain")
+    assert _drain_counts() == (0, 0, 0)
     monkeypatch.delenv("RTW_NO_COOP_SHARE")
     for cap in ("1", "3"):
         monkeypatch.setenv("RTW_MB_CAP", cap)
         assert_bit_identical(shared, R.render(size, 1, 16, 50, world, seed=19), f"{name}: {cap} posts per batch")
+        posted, helped, owned = _drain_counts()
+        assert posted > 0 and posted == helped + owned, (cap, posted, helped, owned)
 
 
 def test_progress_callback_reports_and_keeps_bits(worlds):
@@ -609,3 +643,44 @@ def test_triangle_records_lds_fallback(n_tri, mode2):
     size = R.Size2i(40, 24)
     assert_bit_identical(R.render(size, 1, 4, 50, world, seed=13), O.render(world, R.render_params(size, 4, 50, seed=13)),
                          f"soup {n_tri}")
+
+
+def _sphere_cloud(n: int, seed: int = 3):
+    """n small plain spheres in a slab over a ground sphere (n - 1 spheres + ground = n leaves)."""
+    rng = np.random.default_rng(seed)
+    wb = R.WorldBuilder()
+    mats = [wb.material_lambert_solid((0.7, 0.3, 0.2)), wb.material_metal_solid((0.8, 0.8, 0.8), 0.1),
+            wb.material_dielectric(1.5)]
+    g = wb.new_group()
+    g.add(wb.new_obj_sphere(1000.0, mats[0]).translate((0.0, -1000.0, 0.0)))
+    c = rng.uniform((-8.0, 0.05, -8.0), (8.0, 3.0, 8.0), (n - 1, 3)).astype(np.float32)
+    for i in range(n - 1):
+        g.add(wb.new_obj_sphere(0.04, mats[i % 3]).translate(tuple(float(x) for x in c[i])))
+    cam = R.Camera.build().vertical_fov(50.0, 9.0 / 16.0).position((0.0, 2.0, 10.0)).look_at((0, 1, 0), (0, 1, 0)).build()
+    return g.build().finish(wb, R.BackgroundColor.sky(), cam)
+
+
+@pytest.mark.parametrize("n,folded", [(16384, True), (16385, False)])
+def test_plain_sphere_fold_limit_keeps_sah(n, folded, monkeypatch):
+    """ADVICE r5: the two-children walk's packed node words hold 15-bit children (at most 2^14 leaves);
+    a plain-sphere world one leaf beyond keeps its SAH tree (unfolded records, the triangle loop's
+    one-child walk) instead of silently falling back to the reference tree.  Both sides of the limit
+    render the oracle's bits and the reference-tree loop's."""
+    import torch
+
+    world = _sphere_cloud(n)
+    assert world.raw.leaf_count == n
+    dw = R.DeviceWorld(world, 0)
+    out = torch.empty(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
+    dw.render_into(R.render_params(R.Size2i(16, 16), 1, 50), out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    v = dw.kernel_variant()
+    dw.release()
+    assert v["tree"] == "sah" and v["leaf_kinds"] == (0 if folded else 1), v
+    size = R.Size2i(32, 18)
+    gpu = R.render(size, 1, 2, 50, world, seed=7)
+    assert_bit_identical(gpu, O.render(world, R.render_params(size, 2, 50, seed=7)), f"{n} spheres")
+    big = R.Size2i(160, 90)
+    sah = R.render(big, 1, 2, 50, world, seed=7)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert_bit_identical(sah, R.render(big, 1, 2, 50, world, seed=7), f"{n} spheres: SAH vs reference tree")
