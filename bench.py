@@ -151,11 +151,12 @@ CONFIG_LEGS = (
 
 def _kernel_tag(v: dict) -> str:
     """The render kernel's name fragment in rocprofv3's Kernel_Name for a kernel_variant() dict: the
-    exact template name rtw_world_kernel_name reports (render_kernel<STATS, LDS, LK, TX, GEN>), rebuilt
-    from the fields for a dict without it (a GEN-less name then matches no row: configs_pmc says so)."""
+    exact template name rtw_world_kernel_name reports (render_kernel<STATS, LDS, LK, TX, GEN, WP>), rebuilt
+    from the fields for a dict without it (GEN and WP then taken as false; a wrong guess matches no row and
+    configs_pmc says so)."""
     if v.get("name"):
         return v["name"]
-    return f"render_kernel<false, {v['lds_mode']}, {v['leaf_kinds']}, {v['tex_kinds']}, false>"
+    return f"render_kernel<false, {v['lds_mode']}, {v['leaf_kinds']}, {v['tex_kinds']}, false, false>"
 
 
 def _match_rows(rows, tag: str) -> list:

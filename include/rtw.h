@@ -291,8 +291,9 @@ RTW_API int rtw_world_tuning(rtw_gpu_world* gw, int* trace_min);
  * Diagnostics only. */
 RTW_API int rtw_world_kernel(rtw_gpu_world* gw, int* lds_mode, int* leaf_kinds, int* tex_kinds, int* tree);
 /* The exact template name of that kernel, as profilers print it inside the demangled symbol
- * ("render_kernel<false, 1, 0, 0, false>": counting variant, LDS mode, leaf kinds, texture kinds,
- * generic leaf tables in LDS), NUL-terminated into buf[0..cap); "" before the first render.
+ * ("render_kernel<false, 1, 0, 0, false, false>": counting variant, LDS mode, leaf kinds, texture kinds,
+ * generic leaf tables in LDS, whole-pixel work items), NUL-terminated into buf[0..cap); "" before the
+ * first render.
  * RTW_ERR_INVALID_ARGUMENT if cap is too small.  Diagnostics only (bench.py matches PMC rows by it). */
 RTW_API int rtw_world_kernel_name(rtw_gpu_world* gw, char* buf, int cap);
 /* The shape of this world's last frame (rtw_render_device / rtw_render on it): render-kernel launches,

@@ -527,7 +527,11 @@ __device__ __forceinline__ float d_atanf_x(float x) {
     const float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
     return hx < 0 ? -r : r;
 }
-__device__ __noinline__ float d_acosf(float x) {
+// The sphere uv functions (fdlibm restatements with the exact fast division): inlined into the GEN kernels (the
+// image texture and moving spheres of C5: with calls their texture loop spilled VGPRs to scratch; inlined,
+// earth_motion +1.9 %, 0 scratch, profiles/r06/ab_c5_spills.txt), called out of line elsewhere (inlined into
+// the non-GEN textured kernels: perlin_spheres -3.6 %)
+__device__ __forceinline__ float d_acosf_inl(float x) {
     const float pi = __uint_as_float(0x40490fdau), pio2_hi = __uint_as_float(0x3fc90fdau), pio2_lo = __uint_as_float(0x33a22168u);
     const float pS0 = __uint_as_float(0x3e2aaaabu), pS1 = __uint_as_float(0xbea6b090u), pS2 = __uint_as_float(0x3e4e0aa8u),
                 pS3 = __uint_as_float(0xbd241146u), pS4 = __uint_as_float(0x3a4f7f04u), pS5 = __uint_as_float(0x3811ef08u);
@@ -554,7 +558,7 @@ __device__ __noinline__ float d_acosf(float x) {
     const float c = div_x(z - df * df, s + df);
     return 2.0f * (df + (r * s + c));
 }
-__device__ __noinline__ float d_atan2f(float y, float x) {
+__device__ __forceinline__ float d_atan2f_inl(float y, float x) {
     const float tiny = __uint_as_float(0x0da24260u);
     const float pi_o_4 = __uint_as_float(0x3f490fdbu), pi_o_2 = __uint_as_float(0x3fc90fdbu), pi = __uint_as_float(0x40490fdbu),
                 pi_lo = __uint_as_float(0xb3bbbd2eu);
@@ -583,6 +587,8 @@ __device__ __noinline__ float d_atan2f(float y, float x) {
         default: return (z - pi_lo) - pi;
     }
 }
+__device__ __noinline__ float d_acosf(float x) { return d_acosf_inl(x); }
+__device__ __noinline__ float d_atan2f(float y, float x) { return d_atan2f_inl(y, x); }
 __device__ __noinline__ float d_logf(float x) { return rtw_logf(x); }
 __device__ __noinline__ float d_sinf(float x) { return rtw_sinf(x); }
 
@@ -1003,8 +1009,8 @@ __device__ __forceinline__ void leaf_record(const DWorld& w, int leaf, const Ray
         // of the normal, so skipping it where no image texture can read it changes nothing
         float u = 0.0f, v = 0.0f;
         if (flags & RTW_DLEAF_UV) {
-            const float theta = d_acosf(sn.y);
-            const float phi = d_atan2f(-sn.z, sn.x) + F32_PI;
+            const float theta = TB::gen ? d_acosf_inl(sn.y) : d_acosf(sn.y);
+            const float phi = (TB::gen ? d_atan2f_inl(-sn.z, sn.x) : d_atan2f(-sn.z, sn.x)) + F32_PI;
             u = div_c(phi, F32_TAU, 1.0f / F32_TAU);
             v = div_c(theta, F32_PI, 1.0f / F32_PI);
         }
@@ -1333,7 +1339,10 @@ __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit
         // record (earth_mapped +3 %, perlin_spheres +5 %); the GEN kernels read HBM / L2 (as an LDS table
         // it cost C5 1.3 % in spills, profiles/r05/ab_tex_lds.txt)
         constexpr bool FULL = TX != TX_SOLID && !TB::gen;
-        const int4 t0 = S.tex0 >= 0 ? lds_i4(S.tex0 + (FULL ? 3 * tex : tex)) : w.textures[3 * tex];
+        // GEN kernels with any texture kind get no table from launch_render: no LDS path compiled (with the
+        // inlined uv functions above, earth_motion +1.9 %; alone -2.2 %, profiles/r06/ab_c5_spills.txt)
+        constexpr bool NOTAB = TB::gen && TX != TX_SOLID;
+        const int4 t0 = !NOTAB && S.tex0 >= 0 ? lds_i4(S.tex0 + (FULL ? 3 * tex : tex)) : w.textures[3 * tex];
         const int kind = t0.x;
         if (TX == TX_SOLID || kind == RTW_TEX_SOLID)
             return v3(__int_as_float(t0.y), __int_as_float(t0.z), __int_as_float(t0.w));
@@ -2115,7 +2124,7 @@ __device__ __forceinline__ int mb_take(uint32_t* mb, int v0, int& j) {
     }
 }
 
-template <bool STATS, int LDS, int LK, int TX, bool GEN>
+template <bool STATS, int LDS, int LK, int TX, bool GEN, bool WP>
 __device__ __forceinline__ void render_body(const KArgs& A) {
     constexpr bool LDS_SCENE = LDS >= 1;
     // LDS: [scene: nodes (2 float4 each), leaf records (1 float4 each), cull constants (1 float2
@@ -2266,6 +2275,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     // Worlds of plain spheres and triangles only (leaf kinds 1: meshes that trap paths); elsewhere the
     // code cost more than the drain gained (final_scene1 -0.8 %, cornell_cube -0.6 % with the same 8-way
     // shares: profiles/r05/ab_shared_drain.txt, r5q_part8_coop.txt)
+    // whole-pixel work items (KArgs::whole_pixel) as a compile-time property of the variant: a kernel for
+    // single-sample items carries no whole-pixel code (its SGPR spills 65 -> 56 on final_scene1: +0.4-0.8 %,
+    // suzanne +0.4 %, cornell_cube +0.9 %, profiles/r06/ab_whole_pixel.txt).  The GEN kernels keep the run-time
+    // choice (their WP = false variant serves both): as a template argument their spill layout cost C5 the
+    // 1.2-1.9 % its texture change had gained (ab_whole_pixel.txt, r6e)
+    static_assert(!(GEN && WP), "GEN kernels take whole-pixel items at run time");
+    const bool WPX = GEN ? A.whole_pixel != 0 : WP;
     constexpr bool SHARE_K = !STATS && LDS_SCENE && LK == LK_TRIS;
     int32_t mb_v = SHARE_K ? A.mb_off : -1;
     asm volatile("" : "+v"(mb_v));
@@ -2646,7 +2662,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             T.phase = PH_TRACE;
             if (so.done) {
                 RTW_PT(7);
-                if (A.whole_pixel) {
+                if (WPX) {
                     psum = add(psum, so.color);  // in sample order: this lane renders the pixel's samples in turn
                 } else {
                     float* o = A.colors + ((uint64_t)(sample - A.s_begin) * A.total + slot) * 3;
@@ -2659,7 +2675,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 // slot for the next frame's work order
                 const int32_t bounces = A.max_depth - depth;
                 if (!STATS && A.slot_cost && bounces > 3) {
-                    if (A.whole_pixel) pcost += (uint32_t)bounces;
+                    if (WPX) pcost += (uint32_t)bounces;
                     else atomicAdd(&A.slot_cost[slot], (uint32_t)bounces);
                 }
 #ifdef RTW_WAVE_TIMING
@@ -2672,7 +2688,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 ++sample;
                 if (sample >= sample_end) {
                     T.phase = PH_PIXEL;
-                    if (A.whole_pixel) {  // accumulate_kernel's last step, for this pixel
+                    if (WPX) {  // accumulate_kernel's last step, for this pixel
                         if (!STATS && A.slot_cost && pcost) atomicAdd(&A.slot_cost[slot], pcost);
                         const V3 px = divs(psum, (float)A.spp);
                         float* o = A.layout == RTW_LAYOUT_TILES ? A.out + 3 * (size_t)slot : A.out + 3 * (size_t)pix;
@@ -2744,12 +2760,12 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     }
 }
 
-template <bool STATS, int LDS, int LK, int TX, bool GEN = false>
+template <bool STATS, int LDS, int LK, int TX, bool GEN = false, bool WP = false>
 __global__ __launch_bounds__(RTW_BLOCK, RTW_MIN_WAVES_PER_SIMD) void render_kernel(KArgs A) {
 #ifdef RTW_WAVE_TIMING
     const uint64_t t_start = wall_clock64();
 #endif
-    render_body<STATS, LDS, LK, TX, GEN>(A);
+    render_body<STATS, LDS, LK, TX, GEN, WP>(A);
 #ifdef RTW_WAVE_TIMING
     const uint32_t wv = (blockIdx.x * RTW_BLOCK + threadIdx.x) / 64;
     if ((threadIdx.x & 63) == 0 && wv < 8192) {
@@ -3444,8 +3460,9 @@ struct rtw_gpu_world {
     bool done_recorded = false;
     uint32_t order_tiles = 0;
     bool order_valid = false;      // tile permutation computed for order_key
-    // LDS mode, leaf kinds, texture kinds, tree, GEN (generic leaf tables in LDS) of the last render
-    int32_t last_kernel[5] = {-1, -1, -1, -1, -1};
+    // LDS mode, leaf kinds, texture kinds, tree, GEN (generic leaf tables in LDS), WP (whole-pixel items) of
+    // the last render
+    int32_t last_kernel[6] = {-1, -1, -1, -1, -1, -1};
     // the last frame: render launches, whole-pixel items, the default threshold, in-frame tuning on
     int32_t last_frame[4] = {-1, -1, -1, 0};
 };
@@ -3914,9 +3931,9 @@ extern "C" RTW_API int rtw_world_kernel(rtw_gpu_world* g, int* lds_mode, int* le
 extern "C" RTW_API int rtw_world_kernel_name(rtw_gpu_world* g, char* buf, int cap) {
     if (!g || !buf || cap < 1) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "null argument");
     char s[64] = "";
-    if (g->last_kernel[0] >= 0)  // the product kernel: render_kernel<STATS = false, LDS, LK, TX, GEN>
-        std::snprintf(s, sizeof(s), "render_kernel<false, %d, %d, %d, %s>", g->last_kernel[0], g->last_kernel[1],
-                      g->last_kernel[2], g->last_kernel[4] ? "true" : "false");
+    if (g->last_kernel[0] >= 0)  // the product kernel: render_kernel<STATS = false, LDS, LK, TX, GEN, WP>
+        std::snprintf(s, sizeof(s), "render_kernel<false, %d, %d, %d, %s, %s>", g->last_kernel[0], g->last_kernel[1],
+                      g->last_kernel[2], g->last_kernel[4] ? "true" : "false", g->last_kernel[5] ? "true" : "false");
     if ((int)std::strlen(s) >= cap) return rtw::fail(RTW_ERR_INVALID_ARGUMENT, "buffer too small");
     std::memcpy(buf, s, std::strlen(s) + 1);
     return RTW_OK;
@@ -4123,12 +4140,15 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
         lds += RTW_MB_WORDS * sizeof(uint32_t);
     }
     using KFn = void (*)(KArgs);
-#define RTW_KSET(LK, TX) {render_kernel<false, 0, LK, TX>, render_kernel<false, 1, LK, TX>, render_kernel<false, 2, LK, TX>}
-    static const KFn fns[2][5][3] = {
-        {RTW_KSET(LK_SPHERES, TX_SOLID), RTW_KSET(LK_TRIS, TX_SOLID), RTW_KSET(LK_PLAIN, TX_SOLID),
-         RTW_KSET(LK_WRAPPED, TX_SOLID), RTW_KSET(LK_ANY, TX_SOLID)},
-        {RTW_KSET(LK_SPHERES, TX_ANY), RTW_KSET(LK_TRIS, TX_ANY), RTW_KSET(LK_PLAIN, TX_ANY),
-         RTW_KSET(LK_WRAPPED, TX_ANY), RTW_KSET(LK_ANY, TX_ANY)}};
+    // [whole-pixel items][texture kinds][leaf kinds][LDS mode]
+#define RTW_KSET(LK, TX, WP) \
+    {render_kernel<false, 0, LK, TX, false, WP>, render_kernel<false, 1, LK, TX, false, WP>, render_kernel<false, 2, LK, TX, false, WP>}
+#define RTW_KSET_TX(TX, WP)                                                                                     \
+    {RTW_KSET(LK_SPHERES, TX, WP), RTW_KSET(LK_TRIS, TX, WP), RTW_KSET(LK_PLAIN, TX, WP), RTW_KSET(LK_WRAPPED, TX, WP), \
+     RTW_KSET(LK_ANY, TX, WP)}
+    static const KFn fns[2][2][5][3] = {{RTW_KSET_TX(TX_SOLID, false), RTW_KSET_TX(TX_ANY, false)},
+                                        {RTW_KSET_TX(TX_SOLID, true), RTW_KSET_TX(TX_ANY, true)}};
+#undef RTW_KSET_TX
 #undef RTW_KSET
     static const KFn fns_stats[3] = {render_kernel<true, 0, LK_ANY, TX_ANY>, render_kernel<true, 1, LK_ANY, TX_ANY>,
                                      render_kernel<true, 2, LK_ANY, TX_ANY>};
@@ -4137,21 +4157,26 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
                                             RTW_SSET(LK_WRAPPED)};
 #undef RTW_SSET
     // worlds whose generic leaf tables are in LDS: the GEN variants (leaf kinds 3 and 4, LDS modes 1 and 2)
-    static const KFn fns_gen[2][2][2] = {
-        {{render_kernel<false, 1, LK_WRAPPED, TX_SOLID, true>, render_kernel<false, 2, LK_WRAPPED, TX_SOLID, true>},
-         {render_kernel<false, 1, LK_ANY, TX_SOLID, true>, render_kernel<false, 2, LK_ANY, TX_SOLID, true>}},
-        {{render_kernel<false, 1, LK_WRAPPED, TX_ANY, true>, render_kernel<false, 2, LK_WRAPPED, TX_ANY, true>},
-         {render_kernel<false, 1, LK_ANY, TX_ANY, true>, render_kernel<false, 2, LK_ANY, TX_ANY, true>}}};
+    // (whole-pixel items at run time: render_body's WPX)
+#define RTW_GSET(TX)                                                                                     \
+    {{render_kernel<false, 1, LK_WRAPPED, TX, true>, render_kernel<false, 2, LK_WRAPPED, TX, true>}, \
+     {render_kernel<false, 1, LK_ANY, TX, true>, render_kernel<false, 2, LK_ANY, TX, true>}}
+    static const KFn fns_gen[2][2][2] = {RTW_GSET(TX_SOLID), RTW_GSET(TX_ANY)};
+#undef RTW_GSET
     const bool gen = !stats && A.sh_xf >= 0;  // (the counting variant reads the HBM copies)
+    if (gen && tx != TX_SOLID && A.sh_tex0 >= 0)  // those kernels compile no LDS texture path (texture_sample)
+        return rtw::fail(RTW_ERR_UNSUPPORTED, "GEN kernel with a texture table in LDS");
+    const int wp = A.whole_pixel ? 1 : 0;  // (never in the counting variant, render_frame_body)
     const KFn kf = stats ? (sah ? fns_stats_sah[lk][mode] : fns_stats[mode])
                  : gen   ? fns_gen[tx][lk - LK_WRAPPED][mode - 1]
-                         : fns[tx][lk][mode];
+                         : fns[wp][tx][lk][mode];
     if (!stats) {
         g->last_kernel[0] = mode;
         g->last_kernel[1] = lk;
         g->last_kernel[2] = tx;
         g->last_kernel[3] = sah ? 1 : 0;
         g->last_kernel[4] = gen ? 1 : 0;
+        g->last_kernel[5] = gen ? 0 : wp;  // (the template argument: GEN kernels take either kind of item)
     }
     const void* fn = (const void*)kf;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -42,7 +42,7 @@ def test_config_legs_are_the_baseline_configs():
     assert legs == {("suzanne", 1920, 1080, 512), ("cornell_cube", 800, 800, 1024), ("earth_motion", 3840, 2160, 2048)}
     for (n, w, h, spp, label), cfg in zip(bench.CONFIG_LEGS, (base["configs"][3], base["configs"][2], base["configs"][4])):
         assert f"{w}×{h}" in cfg and f"{spp}spp" in cfg, (label, cfg)
-    assert bench._kernel_tag({"lds_mode": 2, "leaf_kinds": 1, "tex_kinds": 0}) == "render_kernel<false, 2, 1, 0, false>"
+    assert bench._kernel_tag({"lds_mode": 2, "leaf_kinds": 1, "tex_kinds": 0}) == "render_kernel<false, 2, 1, 0, false, false>"
 
 
 def test_kernel_tag_matches_recorded_rocprof_names():
@@ -58,14 +58,16 @@ def test_kernel_tag_matches_recorded_rocprof_names():
     assert len(got) == 1 and "render_kernel<false, 1, 0, 0, false>((anonymous namespace)::KArgs)" in got[0]["Kernel_Name"]
     # the round-5 tag (no GEN argument) matched nothing
     assert bench._match_rows(rows, "render_kernel<false, 1, 0, 0>") == []
-    # a GEN kernel's name differs from its non-GEN sibling's
-    gen = bench._kernel_tag({"lds_mode": 1, "leaf_kinds": 3, "tex_kinds": 1, "name": "render_kernel<false, 1, 3, 1, true>"})
-    assert bench._match_rows([{"Kernel_Name": "void (anonymous namespace)::render_kernel<false, 1, 3, 1, false>(KArgs)"}], gen) == []
+    # a GEN kernel's name differs from its non-GEN sibling's, a whole-pixel kernel's from its single-sample one's
+    gen = bench._kernel_tag({"lds_mode": 1, "leaf_kinds": 3, "tex_kinds": 1, "name": "render_kernel<false, 1, 3, 1, true, true>"})
+    assert bench._match_rows([{"Kernel_Name": "void (anonymous namespace)::render_kernel<false, 1, 3, 1, false, true>(KArgs)"},
+                              {"Kernel_Name": "void (anonymous namespace)::render_kernel<false, 1, 3, 1, true, false>(KArgs)"}],
+                             gen) == []
 
 
 def test_configs_pmc_notes_unmatched_rows(monkeypatch):
     """A config whose kernel has no PMC rows gets roofline None *and* a pmc_note naming what was seen."""
-    rows = [{"Kernel_Name": "void render_kernel<false, 1, 1, 0, false>(KArgs)", "Dispatch_Id": "1",
+    rows = [{"Kernel_Name": "void render_kernel<false, 1, 1, 0, false, false>(KArgs)", "Dispatch_Id": "1",
              "Counter_Name": c, "Counter_Value": "1", "Start_Timestamp": "0", "End_Timestamp": "1"}
             for c in bench.VALU_COUNTERS + ("WRITE_SIZE", "FETCH_SIZE")]
     monkeypatch.setattr(bench, "_pmc_rows", lambda child, counters: rows)
@@ -73,11 +75,11 @@ def test_configs_pmc_notes_unmatched_rows(monkeypatch):
     class A:
         max_depth, seed = 50, 1
 
-    legs = [{"workload": "suzanne", "kernel": {"name": "render_kernel<false, 1, 1, 0, false>"}, "kernel_ms": 1.0,
+    legs = [{"workload": "suzanne", "kernel": {"name": "render_kernel<false, 1, 1, 0, false, false>"}, "kernel_ms": 1.0,
              "colour_record_bytes": 12},
-            {"workload": "earth_motion", "kernel": {"name": "render_kernel<false, 1, 3, 1, true>"}, "kernel_ms": 1.0,
+            {"workload": "earth_motion", "kernel": {"name": "render_kernel<false, 1, 3, 1, true, true>"}, "kernel_ms": 1.0,
              "colour_record_bytes": 12}]
     bench.configs_pmc(A, legs, 1228.8)
     assert legs[0]["roofline"] is not None and legs[0]["roofline"]["traffic"] is not None
     assert "lane_utilisation" in legs[0]["roofline"] and "pmc_note" not in legs[0]
-    assert legs[1]["roofline"] is None and "render_kernel<false, 1, 3, 1, true>" in legs[1]["pmc_note"]
+    assert legs[1]["roofline"] is None and "render_kernel<false, 1, 3, 1, true, true>" in legs[1]["pmc_note"]
