@@ -1612,7 +1612,9 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
 }
 
 // the block-shared drain's traffic (rtw_debug_drain_counts; tests): rays posted to a mailbox, posts traced
-// by another wave of the block, posts traced by their owner (one atomic per batch or ray, drain only)
+// by another wave of the block, posts traced by their owner -- counted in the block's mailbox words 33-35 (LDS
+// atomics) and added here once per block at its end (as one global atomic per post, the counters cost
+// suzanne's 8-way shares 13 %: every block's drain contended on three addresses)
 __device__ unsigned long long rtw_drain_counts[3];
 
 #ifdef RTW_WAVE_TIMING  // experiment builds: per-wave start / end / queue-empty wall clocks of the last launch
@@ -2070,7 +2072,7 @@ __device__ __forceinline__ void coop_apply(Trav& T, int32_t found, float te, boo
 // no lane of the wave is inside a walk), 64 B each: {o, time} {d, fast bits} {inv, -} {answer}.
 // Progress: a helper never waits while holding a taken ray, the owner waits only for rays taken by
 // others, and a helper leaves once `live` is 0 (each wave decrements it once, on its way to helping).
-#define RTW_MB_WORDS 36  // state[16], done[16], live (9 float4)
+#define RTW_MB_WORDS 36  // state[16], done[16], live, the drain counters (rtw_drain_counts) [3] (9 float4)
 template <int LDS, int LK>
 __device__ __forceinline__ float4* mb_slot(int32_t stack_off, int v, int j) {
     // the stack's entry size (traverse's StackEntry): a wave's 64 entries of one level hold ES rays
@@ -2509,7 +2511,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     T.fast &= ~RTW_TF_TIE;
                 }
                 if (lane == 0) {  // the batch's rays are written (release): open it
-                    atomicAdd(&rtw_drain_counts[0], (unsigned long long)post_k);
+                    __hip_atomic_fetch_add(&mb[33], post_k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     const uint32_t s = __hip_atomic_load(&mb[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(&mb[16 + v], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(&mb[v], ((((s >> 16) + 1) & 0xFFFFu) << 16) | (post_k << 8), __ATOMIC_RELEASE,
@@ -2544,7 +2546,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                         if (lane == src) coop_apply(T, h.found, h.te, h.tie);
                     } else if (lane == 0) {
                         mb_answer(mb, mb_slot<LDS, LK>(stack_off, v, j), v, h);
-                        atomicAdd(&rtw_drain_counts[2], 1ull);
+                        __hip_atomic_fetch_add(&mb[35], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
                 if (own) {  // the posts others took: wait for their answers, then every posted lane takes its own
@@ -2730,8 +2732,13 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             const CHit h = coop_solve<LDS, LK>(w, a, A.node_count, A.leaf_count, A.rect_count, A.fast_off, A.coop_ties == 2);
             if (lane == 0) {
                 mb_answer(mb, q, u, h);
-                atomicAdd(&rtw_drain_counts[1], 1ull);
+                __hip_atomic_fetch_add(&mb[34], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+        }
+        __syncthreads();  // (block-uniform branch) every wave's counts are in
+        if (threadIdx.x < 3) {
+            const uint32_t c = __hip_atomic_load(&mb[33 + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (c) atomicAdd(&rtw_drain_counts[threadIdx.x], (unsigned long long)c);
         }
     }
     RTW_PT_FLUSH;

@@ -481,6 +481,11 @@ def test_whole_pixel_items_bit_exact(worlds, name, parts, monkeypatch):
             bufs_r = (fr.image if parts == 1 else fr.tiles).cpu().numpy().copy()
             lf = fr.dworld.last_frame()  # rtw_world_last_frame: one launch of whole-pixel items
             assert lf["whole_pixel"] and lf["launches"] == 1 and lf["trace_min"] == 16, lf
+            # the whole-pixel kernel variant (WP = true), except a GEN kernel: it takes either item kind at run
+            # time (rtw_world_kernel_name: render_kernel<STATS, LDS, LK, TX, GEN, WP>)
+            kname = fr.dworld.kernel_variant()["name"]
+            args = kname[kname.index("<") + 1:-1].split(", ")
+            assert len(args) == 6 and args[0] == "false" and args[5] == ("false" if args[4] == "true" else "true"), kname
             if parts == 1:
                 assert_bit_identical(bufs_r.reshape(-1, 3), ref, f"{name} whole-pixel items")
         bufs.append(bufs_r)
@@ -640,6 +645,8 @@ def test_triangle_records_lds_fallback(n_tri, mode2):
     torch.cuda.synchronize()
     v = dw.kernel_variant()
     assert (v["lds_mode"] == 2) == mode2 and v["lds_mode"] >= 1, v
+    # the exact template name rocprofv3 prints (bench.py matches PMC rows by it): single-sample items, no GEN
+    assert v["name"] == f"render_kernel<false, {v['lds_mode']}, {v['leaf_kinds']}, {v['tex_kinds']}, false, false>", v
     size = R.Size2i(40, 24)
     assert_bit_identical(R.render(size, 1, 4, 50, world, seed=13), O.render(world, R.render_params(size, 4, 50, seed=13)),
                          f"soup {n_tri}")
