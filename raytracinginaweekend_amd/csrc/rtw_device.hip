@@ -1220,18 +1220,22 @@ __device__ __forceinline__ bool node_pass_cons(float4 na, float4 nb, float2 km, 
     const float a1 = na.y - r.o.y, b1 = nb.x - r.o.y;
     const float a2 = na.z - r.o.z, b2 = nb.y - r.o.z;
     const float delta = sah_delta<DQ>(km.x, km.y, a0, b0, a1, b1, a2, b2);
+    // the grown interval's ends per axis, one FMA each: (qa - delta inv, qb + delta inv) is (lo, hi) for inv > 0
+    // and (hi, lo) for inv < 0 (a <= b; fast rays have finite non-zero inv), taken apart by one min and one max.
+    // RN(q -+ delta |inv|) with the product exact differs from RN(q -+ RN(delta |inv|)) only by that
+    // product's rounding, <= u w, far inside the w / 64 the widened constants leave (the containment
+    // argument's real-valued bound holds with the exact product, and RN is monotone)
     const float qa0 = a0 * rp.inv.x, qb0 = b0 * rp.inv.x;
     const float qa1 = a1 * rp.inv.y, qb1 = b1 * rp.inv.y;
     const float qa2 = a2 * rp.inv.z, qb2 = b2 * rp.inv.z;
-    const float w0 = delta * __builtin_fabsf(rp.inv.x), w1 = delta * __builtin_fabsf(rp.inv.y),
-                w2 = delta * __builtin_fabsf(rp.inv.z);
+    const float e00 = __builtin_fmaf(delta, -rp.inv.x, qa0), e10 = __builtin_fmaf(delta, rp.inv.x, qb0);
+    const float e01 = __builtin_fmaf(delta, -rp.inv.y, qa1), e11 = __builtin_fmaf(delta, rp.inv.y, qb1);
+    const float e02 = __builtin_fmaf(delta, -rp.inv.z, qa2), e12 = __builtin_fmaf(delta, rp.inv.z, qb2);
     const float lo = __builtin_fmaxf(
-        __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(qa0, qb0) - w0, __builtin_fminf(qa1, qb1) - w1),
-                        __builtin_fminf(qa2, qb2) - w2),
+        __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(e00, e10), __builtin_fminf(e01, e11)), __builtin_fminf(e02, e12)),
         ts);
     const float hi = __builtin_fminf(
-        __builtin_fminf(__builtin_fminf(__builtin_fmaxf(qa0, qb0) + w0, __builtin_fmaxf(qa1, qb1) + w1),
-                        __builtin_fmaxf(qa2, qb2) + w2),
+        __builtin_fminf(__builtin_fminf(__builtin_fmaxf(e00, e10), __builtin_fmaxf(e01, e11)), __builtin_fmaxf(e02, e12)),
         te);
     entry = lo;  // where the segment enters the grown box: the near-first order of the SAH walk
     return !(lo > hi);

@@ -91,7 +91,8 @@ def test_sah_node_test_contains_exact_cull():
     term, rtw_device.hip node_pass_cons) passes every node that the cull with exact quotients and
     the plain constants passes, on every ray the SAH walk traces (Markstein-exact rays): DESIGN.md
     §5.5's containment argument, checked on 2 M random and special-value cases; for both forms of the
-    delta's k term (mode 2: Dq, round 2's form; mode 3: D^2, the product's)."""
+    delta (mode 2: k Dq + 68u D, round 2's form; mode 3: the product's, k D^2 + 68u D, with the grown
+    interval's ends one FMA each)."""
     for seed, mode in ((21, 2), (22, 2), (23, 3), (24, 3)):
         rng = np.random.default_rng(seed)
         box, ray, rg, km = _cases(rng, 1_000_000, True)
