@@ -4355,7 +4355,14 @@ int render_frame_body(rtw_gpu_world* g, KArgs& A, bool stats, float* out, hipStr
     // A whole-pixel frame keeps its fixed threshold even once an earlier per-sample frame of the world
     // has chosen one: its lanes run whole pixels, not the tuned epochs' single samples.
     A.tune = nullptr;
-    if (!stats && !A.whole_pixel && !std::getenv("RTW_TRACE_MIN")) A.tune = g->tune;
+    // Plain-sphere worlds (the two-children walk) take a fixed threshold of 8 instead of tuning it (round 6):
+    // the tuner chose 6-8 on whole final_scene1 frames but 8-24 on its 8-way shares, whose short epochs picked
+    // 24 on some ranks (that share +3 %); fixed 8 runs within the noise of the best on both
+    // (profiles/r06/ab_trace_min_spheres.txt).  RTW_TUNE_SPHERES=1 keeps the tuner for them.
+    const bool sph_fixed = !stats && !A.whole_pixel && g->leaf_kinds == LK_SPHERES && !std::getenv("RTW_TRACE_MIN") &&
+                           !std::getenv("RTW_TUNE_SPHERES");
+    if (sph_fixed) A.trace_min = 8;
+    if (!stats && !A.whole_pixel && !sph_fixed && !std::getenv("RTW_TRACE_MIN")) A.tune = g->tune;
     // Work order.  A frame renders tiles in the order of the deep-path cost its slots showed in
     // earlier frames of the same partition shape, costliest first, each tile's samples together:
     // the frame then ends on cheap tiles instead of waiting for paths trapped inside a mesh that

@@ -511,9 +511,11 @@ def test_two_children_walk_ties_and_grazing_hits(monkeypatch):
 
 def test_whole_pixel_threshold_stays_fixed_after_tuning(worlds, monkeypatch):
     """a whole-pixel frame runs at its fixed threshold (16) even after a per-sample frame of
-    the same world has tuned one on the device."""
+    the same world has tuned one on the device (plain-sphere worlds keep the tuner only with
+    RTW_TUNE_SPHERES=1; their default is a fixed threshold)."""
     import torch
 
+    monkeypatch.setenv("RTW_TUNE_SPHERES", "1")
     world = worlds("final_scene1")
     dw = R.DeviceWorld(world, 0)
     big = R.render_params(R.Size2i(1920, 1080), 32, 50, seed=3)  # tuning needs >= 26 passes over the slots
@@ -691,3 +693,35 @@ def test_plain_sphere_fold_limit_keeps_sah(n, folded, monkeypatch):
     sah = R.render(big, 1, 2, 50, world, seed=7)
     monkeypatch.setenv("RTW_NO_SAH", "1")
     assert_bit_identical(sah, R.render(big, 1, 2, 50, world, seed=7), f"{n} spheres: SAH vs reference tree")
+
+
+def test_plain_sphere_worlds_take_the_fixed_threshold(worlds, monkeypatch):
+    """Round 6: per-sample frames of plain-sphere worlds run at the fixed threshold 8 without tuning (their
+    8-way shares' short tuning epochs picked 24 on some ranks); RTW_TUNE_SPHERES=1 restores the tuner, and
+    both give the oracle's bits."""
+    import torch
+
+    world = worlds("final_scene1")
+    size = R.Size2i(640, 360)
+    p = R.render_params(size, 8, 50, seed=11)
+    ref = None
+    for tune in (False, True):
+        if tune:
+            monkeypatch.setenv("RTW_TUNE_SPHERES", "1")
+        dw = R.DeviceWorld(world, 0)
+        out = torch.empty(size.count() * 3, dtype=torch.float32, device="cuda:0")
+        dw.render_into(p, out.data_ptr(), 0)
+        torch.cuda.synchronize()
+        lf = dw.last_frame()
+        assert lf["whole_pixel"] == 0, lf
+        if not tune:
+            assert lf["trace_min"] == 8 and dw.tuned_trace_min() == 0, (lf, dw.tuned_trace_min())
+        img = out.cpu().numpy().reshape(-1, 3)
+        if ref is None:
+            ref = img
+        else:
+            assert_bit_identical(img, ref, "tuned vs fixed threshold")
+        dw.release()
+    small = R.Size2i(40, 24)
+    assert_bit_identical(R.render(small, 1, 4, 50, world, seed=11),
+                         O.render(world, R.render_params(small, 4, 50, seed=11)), "fixed threshold")

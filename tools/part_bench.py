@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--max-depth", type=int, default=50)
     ap.add_argument("--ranks", default="ends", help="'ends' (0 and N-1) or 'all'")
+    ap.add_argument("--tile", default="8x8", help="partition tile WxH")
     a = ap.parse_args()
     import torch
 
@@ -29,7 +30,8 @@ def main():
     from raytracinginaweekend_amd.distributed import FrameRenderer, FrameSpec
 
     world = R.demo_world(a.scene)
-    spec = FrameSpec(R.Size2i(a.width, a.height), a.spp, a.max_depth, 0x5EED)
+    spec = FrameSpec(R.Size2i(a.width, a.height), a.spp, a.max_depth, 0x5EED,
+                     tile=tuple(int(x) for x in a.tile.lower().split("x")))
     for n in [int(x) for x in a.parts.split(",")]:
         for rank in (range(n) if a.ranks == "all" else sorted({0, n - 1})):
             fr = FrameRenderer(world, spec, rank, n, 0)
@@ -41,7 +43,7 @@ def main():
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t) / a.steps
             samples = fr.pixels_this_rank() * a.spp
-            print(f"{a.scene} spp={a.spp} depth={a.max_depth} N={n} rank={rank}: {dt * 1e3:.1f} ms/frame, {samples / dt / 1e6:.1f} Msamples/s per rank, "
+            print(f"{a.scene} tile={a.tile} spp={a.spp} depth={a.max_depth} N={n} rank={rank}: {dt * 1e3:.1f} ms/frame, {samples / dt / 1e6:.1f} Msamples/s per rank, "
                   f"x{n} = {n * samples / dt / 1e6:.0f}, trace_min {fr.dworld.tuned_trace_min()}", flush=True)
             del fr
             torch.cuda.empty_cache()
