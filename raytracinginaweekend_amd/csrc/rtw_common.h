@@ -37,6 +37,7 @@ int sah_build(const float* lo, const float* hi, int32_t n, std::vector<rtw_bvh_n
 // references.  Node boxes are the unions of the references' clipped boxes below (rounded outward);
 // km = 2 floats per node, the maxima of the leaf constants below.
 int sah_build_split(const float* lo, const float* hi, const float* tri, const float* leaf_km, int32_t n, double budget,
-                    std::vector<rtw_bvh_node>& nodes, std::vector<float>& km, int32_t* root, int* depth);
+                    std::vector<rtw_bvh_node>& nodes, std::vector<float>& km, int32_t* root, int* depth,
+                    int depth_cap = 0);
 
 }  // namespace rtw

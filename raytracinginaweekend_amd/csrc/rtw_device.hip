@@ -220,7 +220,7 @@ struct KArgs {
     int32_t sh_li, sh_mat, sh_tex0, stack_off;
     int32_t sh_box;  // the leaves' proof boxes (2 float4 each) in LDS after the shading tables, -1: HBM / L2
     int32_t material_count, texture_count;
-    int32_t fast_off;         // LDS float4 offset of the leaf records (leaf_fast)
+    int32_t fast_off;         // LDS float4 offset of leaf 0's record (leaf_fast; held from leaf tri_prefix on)
     int32_t sah;              // 1: hits are found on the SAH tree (node_count = its nodes), verified, and
                               // re-traced on the reference tree where the proof does not hold (§5.6)
     int32_t coop_max;         // drain: a wave with at most this many live lanes traces each ray with all
@@ -250,6 +250,9 @@ struct KArgs {
     // the drain's shared cooperative trace (mb_slot): the block's mailbox words in LDS (float4 offset,
     // -1: each wave traces its own drained rays), and the rays one wave's stack columns hold
     int32_t mb_off, mb_cap;
+    // leaves [0, tri_prefix) are plain triangles with triangle index = leaf index (walk_leaf_record; 0: none), and
+    // the LDS triangle records' component stride (LDS mode 2: the triangle count)
+    int32_t tri_prefix, tri_stride;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -820,19 +823,22 @@ __device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i
     f.y2 = d.w;
     return f;
 }
-// LDS mode 2 keeps the records component-major: component k of triangle i at tf[k * RTW_TRI_SOA + i].
-// With a compile-time stride the four reads share one address register (offsets 0, 16, 32, 48 KB in
-// the ds_read_b128 immediate), and a 16-lane group's reads of one component spread over all 16 slots
-// of the 256-B bank row instead of the 4 that 64-B records start on (4-way conflicts: suzanne's 2.8
-// conflict cycles per LDS instruction in round 2).  Worlds of at most RTW_TRI_SOA triangles.
+// LDS mode 2 keeps the records component-major: component k of triangle i at tf[k * stride + i]: a
+// 16-lane group's reads of one component spread over all 16 slots of the 256-B bank row instead of the 4
+// that 64-B records start on (4-way conflicts: suzanne's 2.8 conflict cycles per LDS instruction in round
+// 2).  The stride: RTW_TRI_SOA records, a compile-time constant whose four reads share one address register
+// (offsets 0, 16, 32, 48 KB in the ds_read_b128 immediate) -- except in the triangle-and-sphere kernels
+// (LK_TRIS), whose stride is the world's triangle count (KArgs::tri_stride): three adds per test, and the
+// 3.5 KB that let suzanne's split tree take mode 2.  (The runtime stride in every kernel cost
+// cornell_cube 2 %, profiles/r06/ab_mode2_suzanne.txt.)
 #ifndef RTW_TRI_SOA
 #define RTW_TRI_SOA 1024
 #endif
 // (Indexing them by leaf instead, and loading a leaf's record with its leaf record before knowing it is a
 // triangle -- one dependent LDS read less per triangle test -- lost 1.8 % on suzanne: the early record's
 // 16 VGPRs; profiles/r04/v5_experiments_ab.txt.)
-__device__ __forceinline__ TriFast load_tri_soa(const float4* __restrict__ tf, int i) {
-    const float4 a = tf[i], b = tf[RTW_TRI_SOA + i], c = tf[2 * RTW_TRI_SOA + i], d = tf[3 * RTW_TRI_SOA + i];
+__device__ __forceinline__ TriFast load_tri_soa(const float4* __restrict__ tf, int i, int32_t stride) {
+    const float4 a = tf[i], b = tf[stride + i], c = tf[2 * stride + i], d = tf[3 * stride + i];
     TriFast f;
     f.p0 = v3(a.x, a.y, a.z);
     f.n = v3(a.w, b.x, b.y);
@@ -1681,28 +1687,48 @@ enum { LK_SPHERES = 0, LK_TRIS = 1, LK_PLAIN = 2, LK_WRAPPED = 3, LK_ANY = 4 };
 __host__ __device__ constexpr int stack_entry_bytes(int lds, int lk) {
     return (lds == 2 || (lds == 1 && lk != LK_SPHERES)) ? 2 : 4;
 }
+// Leaves [0, tri_prefix) of a triangle-and-sphere world (LK_TRIS) are plain triangles with triangle
+// index = leaf index (a mesh's leaves in order: suzanne's 968 of 969, rtw_world_upload): their leaf
+// records are not read -- no dependent LDS read between the walk and the triangle record -- and not held
+// in LDS, whose leaf-record section starts at leaf tri_prefix.  The record such a leaf would have
+// (tag 1, its index in y, w = NaN) is made up instead.  tri_prefix = 0 in other worlds and kernels
+// (rect worlds, LK_PLAIN, take every record: the test cost cornell_cube's leaf-heavy walk 2 %).
+template <int LK>
+__device__ __forceinline__ float4 walk_leaf_record(const float4* __restrict__ fast, int32_t leaf, int32_t tri_prefix) {
+    // (the record read always and the made-up one selected: suzanne -0.4 %, profiles/r06/ab_mode2_suzanne.txt)
+    if (LK == LK_TRIS && leaf < tri_prefix)
+        return make_float4(__int_as_float(1), __int_as_float(leaf), 0.0f, __int_as_float(0x7FC00000));
+    return fast[leaf];
+}
+// the LDS triangle records' stride in kernels of leaf kinds LK (see load_tri_soa)
+template <int LK>
+__device__ __forceinline__ int32_t tri_soa_stride(int32_t tri_stride) {
+    return LK == LK_TRIS ? tri_stride : RTW_TRI_SOA;
+}
 template <bool STATS, int LDS, int LK, bool FAST_ONLY, int TM, class TB>
 __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB& S, Trav T, int32_t trace_min,
-                                      int32_t n_nodes, int32_t n_leaves, int32_t n_rects, int32_t n_tris,
-                                      int32_t stack_off, unsigned long long* dbg, int32_t coop_exit = -1) {
+                                      int32_t n_nodes, int32_t n_leaves, int32_t n_rects, int32_t tri_prefix,
+                                      int32_t tri_stride, int32_t stack_off, unsigned long long* dbg,
+                                      int32_t coop_exit = -1) {
     // the LDS holds the tree this mode walks (the SAH tree in SAH mode); the fallback reads HBM
     constexpr bool LDS_SCENE = LDS >= 1 && TM != TM_FALLBACK;
     constexpr int ACT = TM == TM_FALLBACK ? PH_REF : PH_TRACE;  // the lanes this loop advances
-    (void)n_tris;  // the stack offset comes from the caller
     const DWorld& w = *wp;
     // the plain-triangle records' base, loaded once per call into scalar registers (the world
     // struct is read through a pointer; left in the loop it becomes a dependent global load)
     // LDS: the SAH tree has no cull-constant section (they are in node_b.w)
     constexpr bool C2 = TM == TM_SAH && LK == LK_SPHERES;  // the two-children walk (below)
-    const int32_t rect_off = 2 * n_nodes + n_leaves + (C2 ? 0 : (n_nodes + 1) / 2);
+    // (the LDS leaf records start at leaf tri_prefix, walk_leaf_record)
+    const int32_t rect_off = 2 * n_nodes + n_leaves - tri_prefix + (C2 ? 0 : (n_nodes + 1) / 2);
     const int32_t tri_off = rect_off + 2 * n_rects;
     const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
     const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
     // nodes as two SoA halves (bank-conflict spread of ds_read_b128), then the leaf records
     // The LDS section offsets are held in VGPRs (opaque copies): as SGPRs they compete with the
     // loop's exec masks and get spilled to VGPR lanes, costing a v_readlane per node step.
-    int32_t off_b = n_nodes, off_f = 2 * n_nodes, off_k = 2 * (2 * n_nodes + n_leaves);
+    int32_t off_b = n_nodes, off_f = 2 * n_nodes - tri_prefix, off_k = 2 * (2 * n_nodes + n_leaves - tri_prefix);
     if (LDS_SCENE) asm volatile("" : "+v"(off_b), "+v"(off_f), "+v"(off_k));
+    if (LDS == 2 && LDS_SCENE && LK == LK_TRIS) asm volatile("" : "+v"(tri_stride));
     // the two-children walk's k, also in a VGPR (a scalar would join the spilled SGPRs)
     float sah_k = C2 ? w.sah_k : 0.0f;
     if (C2) asm volatile("" : "+v"(sah_k));
@@ -1763,7 +1789,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB
     const RayPre rp{T.inv, (T.fast & 8) != 0};
     // one leaf's test at the current t range (hittable.rs:436-437: a leaf is never box-tested)
     auto test_leaf = [&](int leaf) {
-        const float4 sph = fast[leaf];
+        const float4 sph = walk_leaf_record<LK>(fast, leaf, tri_prefix);
         if (LK == LK_SPHERES || sph.w == sph.w) {  // a plain sphere
             if (STATS) st.c[ST_T_SPHERE]++;
             float t;
@@ -1781,7 +1807,7 @@ __device__ __forceinline__ Trav traverse(const DWorld* __restrict__ wp, const TB
             if (STATS) st.c[ST_T_TRI]++;
             float t;
             const int ti = __float_as_int(sph.y);
-            if (tri_test(LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), T.ray, 0.001f,
+            if (tri_test(LDS == 2 && LDS_SCENE ? load_tri_soa(tri_fast, ti, tri_soa_stride<LK>(tri_stride)) : load_tri(tri_fast, ti), T.ray, 0.001f,
                          T.te, t))
                 take(t, leaf);
         } else if (LK >= LK_WRAPPED && __float_as_int(sph.x) == 3) {
@@ -1978,10 +2004,12 @@ struct CHit {
 };
 template <int LDS, int LK>
 __device__ __forceinline__ CHit coop_solve(const DWorld& w, const CRay& a, int32_t n_nodes, int32_t n_leaves,
-                                           int32_t n_rects, int32_t fast_off, bool audit) {
+                                           int32_t n_rects, int32_t fast_off, int32_t tri_prefix, int32_t tri_stride,
+                                           bool audit) {
     constexpr bool LDS_SCENE = LDS >= 1;
-    // the SAH tree's LDS scene: plain-sphere worlds have no cull-constant section
-    const int32_t rect_off = 2 * n_nodes + n_leaves + (LK == LK_SPHERES ? 0 : (n_nodes + 1) / 2);
+    // the SAH tree's LDS scene: plain-sphere worlds have no cull-constant section; the leaf records start
+    // at leaf tri_prefix (fast_off is leaf 0's would-be offset, walk_leaf_record)
+    const int32_t rect_off = 2 * n_nodes + n_leaves - tri_prefix + (LK == LK_SPHERES ? 0 : (n_nodes + 1) / 2);
     const int32_t tri_off = rect_off + 2 * n_rects;
     const float4* rects = LDS_SCENE ? smem + rect_off : uniform_ptr(w.rects);
     const float4* tri_fast = LDS == 2 && LDS_SCENE ? smem + tri_off : uniform_ptr(w.tri_fast);
@@ -2007,10 +2035,10 @@ __device__ __forceinline__ CHit coop_solve(const DWorld& w, const CRay& a, int32
     // software-pipelined: the next leaf record is read before this leaf's test, so that its LDS
     // latency overlaps the triangle / rect record read that depends on this one (one round trip per
     // leaf instead of two; the drain's rays are latency-bound)
-    float4 sph_n = lane < n_leaves ? fast[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float4 sph_n = lane < n_leaves ? walk_leaf_record<LK>(fast, lane, tri_prefix) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int32_t leaf = lane; leaf < n_leaves; leaf += 64) {
         const float4 sph = sph_n;
-        if (leaf + 64 < n_leaves) sph_n = fast[leaf + 64];
+        if (leaf + 64 < n_leaves) sph_n = walk_leaf_record<LK>(fast, leaf + 64, tri_prefix);
         float t;
         const float te = best < F32_INF ? __int_as_float(__float_as_int(best) + 1) : F32_INF;
         if (LK == LK_SPHERES || sph.w == sph.w) {
@@ -2022,7 +2050,9 @@ __device__ __forceinline__ CHit coop_solve(const DWorld& w, const CRay& a, int32
             keep(rect_t_mk(g, a.r, a.inv, 0.001f, te, t), t, leaf);  // SAH rays are Markstein-exact
         } else {
             const int ti = __float_as_int(sph.y);
-            keep(tri_test(LDS == 2 ? load_tri_soa(tri_fast, ti) : load_tri(tri_fast, ti), a.r, 0.001f, te, t), t,
+            keep(tri_test(LDS == 2 ? load_tri_soa(tri_fast, ti, tri_soa_stride<LK>(tri_stride)) : load_tri(tri_fast, ti), a.r,
+                          0.001f, te, t),
+                 t,
                  leaf);
         }
     }
@@ -2147,19 +2177,21 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             smem[i] = ga[i];
             smem[A.node_count + i] = gb[i];
         }
-        for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[i];
+        // the leaf records from leaf tri_prefix on (walk_leaf_record)
+        const int32_t n_rec = A.leaf_count - A.tri_prefix;
+        for (int i = threadIdx.x; i < n_rec; i += RTW_BLOCK) smem[2 * A.node_count + i] = w.leaf_fast[A.tri_prefix + i];
         // the cull constants (the plain-sphere worlds' SAH tree keeps them in its node records)
         const bool km_rec = sah && LK == LK_SPHERES;
         const int32_t km_f4 = km_rec ? 0 : (A.node_count + 1) / 2;
-        float2* km = reinterpret_cast<float2*>(smem + 2 * A.node_count + A.leaf_count);
+        float2* km = reinterpret_cast<float2*>(smem + 2 * A.node_count + n_rec);
         const float2* gk = sah ? w.sah_km : w.node_km;
         if (!km_rec)
             for (int i = threadIdx.x; i < A.node_count; i += RTW_BLOCK) km[i] = gk[i];
-        float4* rects = smem + 2 * A.node_count + A.leaf_count + km_f4;
+        float4* rects = smem + 2 * A.node_count + n_rec + km_f4;
         for (int i = threadIdx.x; i < 2 * A.rect_count; i += RTW_BLOCK) rects[i] = w.rects[i];
         if (LDS == 2) {
             float4* tris = rects + 2 * A.rect_count;
-            for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[(i & 3) * RTW_TRI_SOA + (i >> 2)] = w.tri_fast[i];
+            for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[(i & 3) * A.tri_stride + (i >> 2)] = w.tri_fast[i];
         }
         if (A.sh_li >= 0) {  // shading tables (launch_render decides whether they fit)
             int4* li = reinterpret_cast<int4*>(smem + A.sh_li);
@@ -2473,7 +2505,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             uint64_t wx_t0 = wall_clock64();
 #endif
             T = traverse<STATS, LDS, LK, true, TM_SAH>(A.wdev, stabs, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
-                                                       A.leaf_count, A.rect_count, A.tri_count, stack_off,
+                                                       A.leaf_count, A.rect_count, A.tri_prefix, A.tri_stride, stack_off,
                                                        STATS ? A.stats + ST_COUNT : nullptr, dry_coop ? A.coop_max : -1);
             // the rays coop_solve takes (one call site, inlined: as an out-of-line call taking and
             // returning Trav by value it cost 304 B of scratch per lane, saved and restored around
@@ -2545,7 +2577,7 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                     a.inv = v3(__shfl(T.inv.x, src), __shfl(T.inv.y, src), __shfl(T.inv.z, src));
                     a.sgn = __shfl(T.fast, src);
                     const CHit h = coop_solve<LDS, LK>(w, a, A.node_count, A.leaf_count, A.rect_count, A.fast_off,
-                                                       A.coop_ties == 2);
+                                                       A.tri_prefix, A.tri_stride, A.coop_ties == 2);
                     if (!own) {
                         if (lane == src) coop_apply(T, h.found, h.te, h.tie);
                     } else if (lane == 0) {
@@ -2611,18 +2643,18 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
 #endif
             if (__ballot(T.phase == PH_REF) != 0)
                 T = traverse<STATS, LDS, LK, false, TM_FALLBACK>(A.wdev, stabs, T, 0, A.node_count, A.leaf_count, A.rect_count,
-                                                                 A.tri_count, stack_off,
+                                                                 A.tri_prefix, A.tri_stride, stack_off,
                                                                  STATS ? A.stats + ST_COUNT : nullptr);
 #ifdef RTW_WAVE_TIMING
             if (qfail >= RTW_QUEUES) wx_tref += wall_clock64() - wx_t2;
 #endif
         } else if (__ballot(T.phase == PH_TRACE && (T.fast & 8) == 0) == 0) {
             T = traverse<STATS, LDS, LK, true, TM_REF>(A.wdev, stabs, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
-                                               A.leaf_count, A.rect_count, A.tri_count, stack_off,
+                                               A.leaf_count, A.rect_count, A.tri_prefix, A.tri_stride, stack_off,
                                                STATS ? A.stats + ST_COUNT : nullptr);
         } else {
             T = traverse<STATS, LDS, LK, false, TM_REF>(A.wdev, stabs, T, __builtin_amdgcn_readfirstlane(trace_min), A.node_count,
-                                                A.leaf_count, A.rect_count, A.tri_count, stack_off,
+                                                A.leaf_count, A.rect_count, A.tri_prefix, A.tri_stride, stack_off,
                                                 STATS ? A.stats + ST_COUNT : nullptr);
         }
         if (STATS) {
@@ -2733,7 +2765,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             a.r.d = v3(q1.x, q1.y, q1.z);
             a.sgn = __float_as_int(q1.w);
             a.inv = v3(q2.x, q2.y, q2.z);
-            const CHit h = coop_solve<LDS, LK>(w, a, A.node_count, A.leaf_count, A.rect_count, A.fast_off, A.coop_ties == 2);
+            const CHit h = coop_solve<LDS, LK>(w, a, A.node_count, A.leaf_count, A.rect_count, A.fast_off, A.tri_prefix,
+                                               A.tri_stride, A.coop_ties == 2);
             if (lane == 0) {
                 mb_answer(mb, q, u, h);
                 __hip_atomic_fetch_add(&mb[34], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3226,6 +3259,22 @@ int check_world(const rtw_world* w, int* depth_out) {
 // reference tree: when it passes hit_cond at te = succ(t), so do all ancestors (nested, monotone),
 // and the reference DFS reaches the leaf -- whose own Aabb, for a wrapped leaf the apply_aabb
 // quirk's untransformed box, need not hold the hit at all.
+// the length of the world's leading run of plain triangle leaves whose triangle index is their leaf index
+// (walk_leaf_record; a mesh added first, as in suzanne, or a triangle soup)
+int32_t tri_prefix_of(const rtw_world* w) {
+    int32_t p = 0;
+    while (p < w->leaf_count && w->leaves[p].geom_kind == RTW_GEOM_TRIANGLE && w->leaves[p].flags == 0 &&
+           w->leaves[p].geom_index == p)
+        ++p;
+    return p;
+}
+// LDS bytes of mode 2 for the one-child walk's tables (launch_render's sizing: nodes, the leaf records from
+// the triangle prefix on, cull constants, rect records, triangle records at the exact stride, 16-bit stack
+// of `depth` entries, the drain's mailbox) -- the depth cap of the split tree (build_sah_tables) aims at it
+size_t lds_mode2_bytes(size_t nodes, size_t leaf_records, size_t rects, size_t tris, int depth) {
+    return (2 * nodes + leaf_records + (nodes + 1) / 2 + 2 * rects + 4 * tris) * sizeof(float4) +
+           (size_t)depth * RTW_BLOCK * sizeof(int16_t) + RTW_MB_WORDS * sizeof(uint32_t);
+}
 struct SahTables {
     std::vector<float4> a, b;     // nodes, as node_a / node_b
     std::vector<float> km;        // cull constants, 2 per node
@@ -3310,11 +3359,54 @@ SahTables build_sah_tables(const rtw_world* w) {
         std::vector<float> skm;
         int32_t sroot = 0;
         int sdepth = 0;
-        bool ok = rtw::sah_build_split(lo.data(), hi.data(), tri.data(), lkm.data(), L, budget, split, skm, &sroot, &sdepth) == 0 &&
+        const char* cap_env = std::getenv("RTW_SAH_DEPTH_CAP");  // tests / audits: this cap (0: none)
+        bool ok = rtw::sah_build_split(lo.data(), hi.data(), tri.data(), lkm.data(), L, budget, split, skm, &sroot, &sdepth,
+                                       cap_env ? std::atoi(cap_env) : 0) == 0 &&
                   sdepth <= RTW_STACK;
         for (const rtw_bvh_node& nd : split)
             for (int k2 = 0; k2 < 3; ++k2)
                 if (!coord_ok(nd.min[k2]) || !coord_ok(nd.max[k2])) ok = false;
+        // The depth cap: a split tree whose 16-bit stack keeps it out of LDS mode 2 (the triangle records in
+        // LDS) is rebuilt with the largest depth cap that lets it in, down to ceil(log2 L) + 5 levels (worlds
+        // of plain triangles and spheres: the LK_TRIS kernels' layout, lds_mode2_bytes).
+        // suzanne: depth 21 -> 16, 1770 -> 1719 nodes, node tests per ray +0.5 %, leaf tests +1.7 %
+        // (tools/sah_cost.py), and the triangle records in LDS: DESIGN 5.3.
+        bool tris_spheres = true;  // the kernels with the exact triangle stride and the prefix (LK_TRIS)
+        for (int32_t i = 0; i < L; ++i)
+            if ((w->leaves[i].geom_kind != RTW_GEOM_TRIANGLE && w->leaves[i].geom_kind != RTW_GEOM_SPHERE) ||
+                w->leaves[i].flags != 0)
+                tris_spheres = false;
+        if (ok && !cap_env && tris_spheres && L < 32768) {
+            int rdepth = 0;
+            check_world(w, &rdepth);
+            const size_t P = (size_t)tri_prefix_of(w);
+            auto fits2 = [&](size_t n, int d) {
+                return n < 32768 && lds_mode2_bytes(n, (size_t)L - P, (size_t)w->rect_count, (size_t)w->triangle_count,
+                                                    std::max(d, rdepth)) <= RTW_LDS_SCENE_MAX;
+            };
+            int lb = 5;
+            while ((1 << (lb - 5)) < L) ++lb;
+            if (!fits2(split.size(), sdepth) && fits2((size_t)L - 1, lb))
+                for (int c = sdepth - 1; c >= lb; --c) {
+                    std::vector<rtw_bvh_node> s2;
+                    std::vector<float> k2v;
+                    int32_t r2 = 0;
+                    int d2 = 0;
+                    if (rtw::sah_build_split(lo.data(), hi.data(), tri.data(), lkm.data(), L, budget, s2, k2v, &r2, &d2, c) != 0)
+                        break;
+                    bool ok2 = d2 <= c;
+                    for (const rtw_bvh_node& nd : s2)
+                        for (int k3 = 0; k3 < 3; ++k3)
+                            if (!coord_ok(nd.min[k3]) || !coord_ok(nd.max[k3])) ok2 = false;
+                    if (ok2 && fits2(s2.size(), d2)) {
+                        split.swap(s2);
+                        skm.swap(k2v);
+                        sroot = r2;
+                        sdepth = d2;
+                        break;
+                    }
+                }
+        }
         // The extra nodes must not push the world out of the LDS modes (launch_render: mode 1 holds
         // nodes, leaf records, cull constants, rects and the 16-bit stack, mode 2 the triangle records
         // too): a split tree that fits mode 1 only beats the object-split tree in mode 2 (suzanne at
@@ -3452,6 +3544,7 @@ struct rtw_gpu_world {
     int32_t node_count = 0, leaf_count = 0, depth = 1;
     int32_t tri_count = 0, rect_count = 0, material_count = 0, texture_count = 0, sphere_count = 0, box_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
+    int32_t tri_prefix = 0;  // leaves [0, tri_prefix): plain triangles, triangle index = leaf index (walk_leaf_record)
     int32_t sah_nodes = 0;  // nodes of the SAH tree, 0: the world takes the reference tree only (§5.6)
     bool sah_folded = false;  // its node records are the two-children walk's (plain-sphere worlds)
     int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
@@ -3764,6 +3857,7 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         g->depth = std::max(g->depth, sah.depth);
     }
     g->tri_count = w->triangle_count;
+    g->tri_prefix = tri_prefix_of(w);
     g->rect_count = w->rect_count;
     g->sphere_count = w->sphere_count;
     g->box_count = w->box_count;
@@ -4072,25 +4166,30 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
 #ifdef RTW_PHASE_TIMING
     cap -= (RTW_BLOCK / 64) * 10 * sizeof(unsigned long long);  // the per-wave phase sums (pt_slot)
 #endif
-    const size_t tri_bytes = (size_t)4 * RTW_TRI_SOA * sizeof(float4);  // mode 2: component-major, fixed stride
     const size_t stack_bytes = (size_t)g->depth * RTW_BLOCK * sizeof(int32_t);
     const size_t stack16_bytes = stack_bytes / 2;  // 16-bit entries
     const char* lds_mode_env = std::getenv("RTW_LDS_MODE");  // audits: cap the mode
     A.node_count = sah ? g->sah_nodes : g->node_count;
-    // LDS scene: [node_a n][node_b n][leaf records L][cull constants (n + 1) / 2, reference tree only][rects
-    // 2R] (+ the triangle records in mode 2)
+    // the LK template argument of the kernel launch_render picks below (the counting variant of a world
+    // without the SAH walk runs the LK_ANY loop): its stack entries are the ones the LDS must hold, and
+    // only its triangle loops skip the triangle prefix's leaf records (walk_leaf_record)
+    const int kernel_lk = stats && !sah ? (int)LK_ANY : lk;
+    A.tri_prefix = kernel_lk == LK_TRIS ? g->tri_prefix : 0;
+    A.tri_stride = kernel_lk == LK_TRIS ? std::max(1, g->tri_count) : RTW_TRI_SOA;  // tri_soa_stride
+    const size_t tri_bytes = (size_t)4 * A.tri_stride * sizeof(float4);  // mode 2: component-major (load_tri_soa)
+    // LDS scene: [node_a n][node_b n][leaf records L - tri_prefix][cull constants (n + 1) / 2, not in the
+    // plain-sphere SAH tree][rects 2R] (+ the triangle records in mode 2)
     const size_t scene_bytes =
-        (size_t)(2 * A.node_count + g->leaf_count + (sah && lk == LK_SPHERES ? 0 : (A.node_count + 1) / 2) +
+        (size_t)(2 * A.node_count + g->leaf_count - A.tri_prefix + (sah && lk == LK_SPHERES ? 0 : (A.node_count + 1) / 2) +
                  2 * g->rect_count) * sizeof(float4);
-    A.fast_off = 2 * A.node_count;
+    A.fast_off = 2 * A.node_count - A.tri_prefix;  // where leaf 0's record would be
+    if (A.fast_off < 0) return rtw::fail(RTW_ERR_UNSUPPORTED, "triangle prefix longer than the node records");
     int mode = 0;
     // 16-bit stack entries (traverse's StackEntry): worlds of < 2^15 nodes (both trees) and leaves
     const bool small = g->leaf_count < 32768 && A.node_count < 32768 && g->node_count < 32768;
-    // the LK template argument of the kernel launch_render picks below (the counting variant of a world
-    // without the SAH walk runs the LK_ANY loop): its stack entries are the ones the LDS must hold
-    const int kernel_lk = stats && !sah ? (int)LK_ANY : lk;
     const size_t stack1_bytes = (size_t)stack_entry_bytes(1, kernel_lk) * g->depth * RTW_BLOCK;  // mode 1
-    if (g->tri_count > 0 && g->tri_count <= RTW_TRI_SOA && small && scene_bytes + tri_bytes + stack16_bytes <= cap)
+    if (g->tri_count > 0 && g->tri_count <= A.tri_stride && small &&
+        scene_bytes + tri_bytes + stack16_bytes + RTW_MB_WORDS * sizeof(uint32_t) <= cap)
         mode = 2;
     else if (scene_bytes + stack1_bytes <= cap && (small || stack_entry_bytes(1, kernel_lk) == 4)) mode = 1;
     if (lds_mode_env) mode = std::min(mode, std::atoi(lds_mode_env));
@@ -4123,7 +4222,8 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     // ... and the generic leaf path's transforms, spheres and boxes (worlds with wrapped or box leaves, or
     // volumes; RTW_NO_GEN_LDS=1 keeps them in HBM / L2)
     A.sh_xf = A.sh_sph = A.sh_bx = -1;
-    A.sh_rect = mode >= 1 ? 2 * A.node_count + g->leaf_count + (sah && lk == LK_SPHERES ? 0 : (A.node_count + 1) / 2) : -1;
+    A.sh_rect = mode >= 1 ? 2 * A.node_count + g->leaf_count - A.tri_prefix + (sah && lk == LK_SPHERES ? 0 : (A.node_count + 1) / 2)
+                          : -1;
     const size_t gen_bytes = (size_t)(3 * g->leaf_count + g->sphere_count + 2 * g->box_count) * sizeof(float4);
     if (sh && lk >= LK_WRAPPED && lds + gen_bytes <= cap && !(ngl && ngl[0] && ngl[0] != '0')) {
         A.sh_xf = A.stack_off;

@@ -169,6 +169,7 @@ struct SplitBuilder {
     std::vector<rtw_bvh_node>* nodes;
     std::vector<float>* km;  // 2 per node: the maxima over the leaves below
     int max_depth = 0;
+    int depth_cap = 0;  // > 0: no leaf deeper (children of a node at depth d hold <= 2^(cap - d - 1) references)
     bool bad = false;  // a reference box came out empty or not finite: the caller takes the object-split tree
     struct Out {
         int32_t id;
@@ -267,6 +268,10 @@ struct SplitBuilder {
                 clo[k] = std::min(clo[k], c);
                 chi[k] = std::max(chi[k], c);
             }
+        // the depth cap: each child of this node holds at most lim references (a median split always
+        // does, by induction from the root's n <= 2^cap)
+        const size_t lim = depth_cap > 0 && depth_cap - depth - 1 < 62 ? (size_t)1 << std::max(0, depth_cap - depth - 1)
+                                                                      : SIZE_MAX;
         // object split: binned SAH over the centres
         double best = INFINITY;
         int axis = -1, best_bin = -1;
@@ -295,7 +300,7 @@ struct SplitBuilder {
                 for (int b = 0; b < kSBins - 1; ++b) {
                     for (int j = 0; j < 3; ++j) ll[j] = std::min(ll[j], bl[b][j]), lh[j] = std::max(lh[j], bh[b][j]);
                     ln += cnt[b];
-                    if (ln == 0 || ln == n) continue;
+                    if (ln == 0 || ln == n || ln > lim || n - ln > lim) continue;
                     const double c = area(ll, lh) * (double)ln + rc[b + 1];
                     if (c < best) best = c, axis = k, best_bin = b;
                 }
@@ -342,7 +347,8 @@ struct SplitBuilder {
                     for (int j = 0; j < 3; ++j) ll[j] = std::min(ll[j], bl[b][j]), lh[j] = std::max(lh[j], bh[b][j]);
                     ln += enter[b];
                     rn2 -= leave[b];
-                    if (ln == 0 || rn2 == 0 || ln == n || rn2 == n || (int64_t)(ln + rn2 - n) > extra) continue;
+                    if (ln == 0 || rn2 == 0 || ln == n || rn2 == n || (int64_t)(ln + rn2 - n) > extra || ln > lim || rn2 > lim)
+                        continue;
                     const double c = area(ll, lh) * (double)ln + rc[b + 1];
                     if (c < sbest) sbest = c, saxis = k, splane = pos(b + 1);
                 }
@@ -367,7 +373,7 @@ struct SplitBuilder {
                 }
             }
             if (left.empty() || right.empty() || left.size() == n || right.size() == n ||
-                (int64_t)(left.size() + right.size() - n) > extra) {
+                (int64_t)(left.size() + right.size() - n) > extra || left.size() > lim || right.size() > lim) {
                 left.clear();
                 right.clear();
             } else {
@@ -383,7 +389,7 @@ struct SplitBuilder {
                     (b <= best_bin ? left : right).push_back(r);
                 }
             }
-            if (left.empty() || right.empty()) {  // median split on the widest centre axis
+            if (left.empty() || right.empty() || left.size() > lim || right.size() > lim) {  // median split on the widest centre axis
                 left.clear();
                 right.clear();
                 axis = 0;
@@ -429,7 +435,7 @@ struct SplitBuilder {
 namespace rtw {
 
 int sah_build_split(const float* lo, const float* hi, const float* tri, const float* leaf_km, int32_t n, double budget,
-                    std::vector<rtw_bvh_node>& nodes, std::vector<float>& km, int32_t* root, int* depth) {
+                    std::vector<rtw_bvh_node>& nodes, std::vector<float>& km, int32_t* root, int* depth, int depth_cap) {
     nodes.clear();
     km.clear();
     if (n <= 1) return -1;
@@ -445,6 +451,8 @@ int sah_build_split(const float* lo, const float* hi, const float* tri, const fl
     B.tri = tri;
     B.lkm = leaf_km;
     B.extra = (int64_t)(budget * n);
+    // a cap the root's references cannot meet is no cap (median splits need n <= 2^cap)
+    B.depth_cap = depth_cap > 0 && depth_cap < 62 && (int64_t)n <= ((int64_t)1 << depth_cap) ? depth_cap : 0;
     B.nodes = &nodes;
     B.km = &km;
     nodes.reserve((size_t)n + (size_t)B.extra);

@@ -617,6 +617,30 @@ def test_suzanne_large_split_budget_bit_exact(worlds, monkeypatch):
     assert_bit_identical(sah, R.render(big, 1, 8, 50, world, seed=29), "suzanne split budget 4 vs reference tree")
 
 
+def test_suzanne_depth_capped_tree_in_lds_mode2(worlds, monkeypatch):
+    """suzanne's split tree, rebuilt under the depth cap that lets its 16-bit stack, nodes and triangle records
+    share the 160 KB (build_sah_tables), runs LDS mode 2 with the mesh's leaf records left out (leaf_record:
+    its 968 triangles are leaves 0..967); bit-exact against the oracle.  A far tighter cap (11 levels: median
+    splits under most of the tree) must give the reference tree's bits too."""
+    import torch
+
+    world = worlds("suzanne")
+    dw = R.DeviceWorld(world, 0)
+    out = torch.empty(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
+    dw.render_into(R.render_params(R.Size2i(16, 16), 1, 50), out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    v = dw.kernel_variant()
+    assert v["lds_mode"] == 2 and v["tree"].startswith("sah") and v["leaf_kinds"] == 1, v
+    size = R.Size2i(48, 36)
+    assert_bit_identical(R.render(size, 1, 4, 50, world, seed=7), O.render(world, R.render_params(size, 4, 50, seed=7)),
+                         "suzanne, depth-capped tree, mode 2")
+    monkeypatch.setenv("RTW_SAH_DEPTH_CAP", "11")
+    big = R.Size2i(320, 180)
+    sah = R.render(big, 1, 8, 50, world, seed=5)
+    monkeypatch.setenv("RTW_NO_SAH", "1")
+    assert_bit_identical(sah, R.render(big, 1, 8, 50, world, seed=5), "suzanne cap 11 vs reference tree")
+
+
 def _soup_world(n_tri: int, seed: int = 5):
     """A random triangle soup over a ground sphere (mesh worlds of any size)."""
     rng = np.random.default_rng(seed)
@@ -633,11 +657,12 @@ def _soup_world(n_tri: int, seed: int = 5):
     return g.build().finish(wb, R.BackgroundColor.sky(), cam)
 
 
-@pytest.mark.parametrize("n_tri,mode2", [(300, True), (1100, False)])
+@pytest.mark.parametrize("n_tri,mode2", [(300, True), (1100, True), (2000, False)])
 def test_triangle_records_lds_fallback(n_tri, mode2):
-    """LDS mode 2 holds the triangle records component-major with a fixed 1024-record stride
-    (RTW_TRI_SOA); a mesh world above it falls back to mode 1 (records from L2), which
-    rtw_world_kernel reports, and both render the oracle's bits."""
+    """LDS mode 2 holds the triangle records component-major at the world's own stride (its triangle
+    count: 1100 triangles fit, the 1024-record limit of rounds 2-5 is gone); a mesh world whose records
+    do not fit falls back to mode 1 (records from L2), which rtw_world_kernel reports, and both render
+    the oracle's bits."""
     import torch
 
     world = _soup_world(n_tri)
