@@ -253,6 +253,7 @@ struct KArgs {
     // leaves [0, tri_prefix) are plain triangles with triangle index = leaf index (walk_leaf_record; 0: none), and
     // the LDS triangle records' component stride (LDS mode 2: the triangle count)
     int32_t tri_prefix, tri_stride;
+    int32_t tri_prefix_mat, tri_prefix_w;  // the prefix leaves' material and leaf_info.w (ShadeTabsT PRE)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -647,11 +648,14 @@ struct Stats {
 // leaves): as runtime choices their loads became pointer selects and flat loads, and their offsets
 // occupied SGPRs across the bounce loop (suzanne -3 % from the spills).
 extern __shared__ __attribute__((aligned(16))) float4 smem[];
-template <bool GEN, bool RECT>
+// PRE (the LK_TRIS kernels): leaves [0, pre) are the triangle prefix (walk_leaf_record), whose leaf_info
+// is made up from the prefix's one material and flags word -- the LDS table holds the other leaves only
+template <bool GEN, bool RECT, bool PRE = false>
 struct ShadeTabsT {
     int32_t li, mat, tex0, fast;
     int32_t xf, sph, bx, rect;  // leaf_xf, spheres, boxes (GEN), rects (RECT)
-    static constexpr bool gen = GEN, rect_lds = RECT;
+    int32_t pre, pre_mat, pre_w;  // PRE: the prefix's length, material and leaf_info.w
+    static constexpr bool gen = GEN, rect_lds = RECT, prefix = PRE;
 };
 using ShadeTabs = ShadeTabsT<false, false>;  // the tables of the device self-test kernels
 __device__ __forceinline__ int4 lds_i4(int32_t i) { return reinterpret_cast<const int4*>(smem)[i]; }
@@ -663,6 +667,8 @@ __device__ __forceinline__ float4 tab_gen(const TB& S, int32_t off, const float4
 }
 template <class TB>
 __device__ __forceinline__ int4 leaf_info_of(const DWorld& w, const TB& S, int leaf) {
+    if constexpr (TB::prefix)
+        if (leaf < S.pre) return make_int4(RTW_GEOM_TRIANGLE, leaf, S.pre_mat, S.pre_w);
     int4 v;
     if (S.li >= 0) v = lds_i4(S.li + leaf);
     else v = w.leaf_info[leaf];
@@ -2194,8 +2200,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
             for (int i = threadIdx.x; i < 4 * A.tri_count; i += RTW_BLOCK) tris[(i & 3) * A.tri_stride + (i >> 2)] = w.tri_fast[i];
         }
         if (A.sh_li >= 0) {  // shading tables (launch_render decides whether they fit)
-            int4* li = reinterpret_cast<int4*>(smem + A.sh_li);
-            for (int i = threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) li[i] = w.leaf_info[i];
+            int4* li = reinterpret_cast<int4*>(smem + A.sh_li);  // from leaf tri_prefix on (leaf_info_of)
+            for (int i = A.tri_prefix + threadIdx.x; i < A.leaf_count; i += RTW_BLOCK) li[i] = w.leaf_info[i];
             int4* mt = reinterpret_cast<int4*>(smem + A.sh_mat);
             for (int i = threadIdx.x; i < A.material_count; i += RTW_BLOCK) mt[i] = w.materials[i];
             if (A.sh_box >= 0)
@@ -2226,11 +2232,14 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
     const int32_t stack_off = LDS_SCENE ? A.stack_off : 0;
     // the generic tables only where the world's leaf kinds can read them (compile-time -1 elsewhere: their
     // offsets would otherwise occupy SGPRs across the bounce loop, which spills -- suzanne -3 %)
-    ShadeTabsT<GEN, LDS_SCENE && LK >= LK_PLAIN> stabs{A.sh_li, A.sh_mat, A.sh_tex0, A.sh_li >= 0 ? A.fast_off : -1,
-                                                       GEN ? A.sh_xf : -1, GEN ? A.sh_sph : -1, GEN ? A.sh_bx : -1,
-                                                       LDS_SCENE && LK >= LK_PLAIN ? A.sh_rect : -1};
+    ShadeTabsT<GEN, LDS_SCENE && LK >= LK_PLAIN, LK == LK_TRIS> stabs{
+        A.sh_li, A.sh_mat, A.sh_tex0, A.sh_li >= 0 ? A.fast_off : -1,
+        GEN ? A.sh_xf : -1, GEN ? A.sh_sph : -1, GEN ? A.sh_bx : -1,
+        LDS_SCENE && LK >= LK_PLAIN ? A.sh_rect : -1,
+        LK == LK_TRIS ? A.tri_prefix : 0, A.tri_prefix_mat, A.tri_prefix_w};
     // the shading tables' offsets in VGPRs: as SGPRs they are live across the bounce loop and spill
     asm volatile("" : "+v"(stabs.li), "+v"(stabs.mat), "+v"(stabs.tex0), "+v"(stabs.fast));
+    if (LK == LK_TRIS) asm volatile("" : "+v"(stabs.pre), "+v"(stabs.pre_mat), "+v"(stabs.pre_w));
     Stats st;
     if (STATS)
         for (int i = 0; i < ST_COUNT; ++i) st.c[i] = 0;
@@ -3260,11 +3269,12 @@ int check_world(const rtw_world* w, int* depth_out) {
 // and the reference DFS reaches the leaf -- whose own Aabb, for a wrapped leaf the apply_aabb
 // quirk's untransformed box, need not hold the hit at all.
 // the length of the world's leading run of plain triangle leaves whose triangle index is their leaf index
-// (walk_leaf_record; a mesh added first, as in suzanne, or a triangle soup)
+// (walk_leaf_record; a mesh added first, as in suzanne, or a triangle soup) ...
+// and whose material is leaf 0's (leaf_info_of makes their leaf_info up)
 int32_t tri_prefix_of(const rtw_world* w) {
     int32_t p = 0;
     while (p < w->leaf_count && w->leaves[p].geom_kind == RTW_GEOM_TRIANGLE && w->leaves[p].flags == 0 &&
-           w->leaves[p].geom_index == p)
+           w->leaves[p].geom_index == p && w->leaves[p].material == w->leaves[0].material)
         ++p;
     return p;
 }
@@ -3545,6 +3555,7 @@ struct rtw_gpu_world {
     int32_t tri_count = 0, rect_count = 0, material_count = 0, texture_count = 0, sphere_count = 0, box_count = 0;
     int32_t mk_world = 0;  // every node coordinate is 0 or >= 2^-60 in magnitude (ray_pre)
     int32_t tri_prefix = 0;  // leaves [0, tri_prefix): plain triangles, triangle index = leaf index (walk_leaf_record)
+    int32_t tri_prefix_mat = 0, tri_prefix_w = 0;  // their material and leaf_info.w (leaf_info_of)
     int32_t sah_nodes = 0;  // nodes of the SAH tree, 0: the world takes the reference tree only (§5.6)
     bool sah_folded = false;  // its node records are the two-children walk's (plain-sphere worlds)
     int32_t leaf_kinds = LK_ANY;  // LK_*: the traversal loop the world's leaves need
@@ -3858,6 +3869,10 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     }
     g->tri_count = w->triangle_count;
     g->tri_prefix = tri_prefix_of(w);
+    if (g->tri_prefix > 0) {
+        g->tri_prefix_mat = li[0].z;
+        g->tri_prefix_w = li[0].w;
+    }
     g->rect_count = w->rect_count;
     g->sphere_count = w->sphere_count;
     g->box_count = w->box_count;
@@ -4201,12 +4216,22 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const char* ngl = std::getenv("RTW_NO_GEN_LDS");
     const bool gen_wanted = !stats && lk >= LK_WRAPPED && !(ngl && ngl[0] && ngl[0] != '0');
     const int tex_recs = (stats || tx != TX_SOLID) ? (gen_wanted ? 0 : 3) : 1;
-    const size_t sh_bytes = (size_t)(g->leaf_count + A.material_count + tex_recs * A.texture_count) * sizeof(int4);
+    // (the leaf_info table from leaf tri_prefix on: the prefix's is made up, leaf_info_of)
+    const int32_t n_li = g->leaf_count - A.tri_prefix;
+    const size_t sh_bytes = (size_t)(n_li + A.material_count + tex_recs * A.texture_count) * sizeof(int4);
     const char* nsl = std::getenv("RTW_NO_SHADE_LDS");
-    const bool sh = mode >= 1 && lds + sh_bytes <= cap && !(nsl && nsl[0] && nsl[0] != '0');
-    A.sh_li = sh ? scene_f4 : -1;
-    A.sh_mat = sh ? scene_f4 + g->leaf_count : -1;
-    A.sh_tex0 = sh && tex_recs > 0 && A.texture_count > 0 ? scene_f4 + g->leaf_count + A.material_count : -1;
+    const char* ncs = std::getenv("RTW_NO_COOP_SHARE");
+    // the shared drain's mailbox (below) keeps its 144 B ahead of the tables
+    const bool mb_want = !stats && mode >= 1 && sah && lk == LK_TRIS && A.coop_max > 0 && g->depth >= 1 &&
+                         !(ncs && ncs[0] && ncs[0] != '0');
+    const size_t mb_bytes = mb_want ? RTW_MB_WORDS * sizeof(uint32_t) : 0;
+    const bool sh = mode >= 1 && lds + sh_bytes + mb_bytes <= cap && !(nsl && nsl[0] && nsl[0] != '0');
+    A.sh_li = sh ? scene_f4 - A.tri_prefix : -1;
+    if (sh && A.sh_li < 0) return rtw::fail(RTW_ERR_UNSUPPORTED, "triangle prefix longer than the LDS scene");
+    A.sh_mat = sh ? scene_f4 + n_li : -1;
+    A.sh_tex0 = sh && tex_recs > 0 && A.texture_count > 0 ? scene_f4 + n_li + A.material_count : -1;
+    A.tri_prefix_mat = A.tri_prefix > 0 ? g->tri_prefix_mat : 0;
+    A.tri_prefix_w = A.tri_prefix > 0 ? g->tri_prefix_w : 0;
     A.stack_off = scene_f4 + (sh ? (int32_t)(sh_bytes / sizeof(int4)) : 0);
     if (sh) lds += sh_bytes;
     // ... and the SAH walk's proof boxes (one read per traced ray, else a dependent L2 read between the
@@ -4214,7 +4239,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     const size_t box_bytes = (size_t)g->leaf_count * 2 * sizeof(float4);
     const char* npl = std::getenv("RTW_NO_PROOF_LDS");
     A.sh_box = -1;
-    if (sh && sah && g->w.leaf_box && lds + box_bytes <= cap && !(npl && npl[0] && npl[0] != '0')) {
+    if (sh && sah && g->w.leaf_box && lds + box_bytes + mb_bytes <= cap && !(npl && npl[0] && npl[0] != '0')) {
         A.sh_box = A.stack_off;
         A.stack_off += (int32_t)(box_bytes / sizeof(float4));
         lds += box_bytes;
@@ -4225,7 +4250,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     A.sh_rect = mode >= 1 ? 2 * A.node_count + g->leaf_count - A.tri_prefix + (sah && lk == LK_SPHERES ? 0 : (A.node_count + 1) / 2)
                           : -1;
     const size_t gen_bytes = (size_t)(3 * g->leaf_count + g->sphere_count + 2 * g->box_count) * sizeof(float4);
-    if (sh && lk >= LK_WRAPPED && lds + gen_bytes <= cap && !(ngl && ngl[0] && ngl[0] != '0')) {
+    if (sh && lk >= LK_WRAPPED && lds + gen_bytes + mb_bytes <= cap && !(ngl && ngl[0] && ngl[0] != '0')) {
         A.sh_xf = A.stack_off;
         A.sh_sph = A.sh_xf + 3 * g->leaf_count;
         A.sh_bx = A.sh_sph + g->sphere_count;
@@ -4241,9 +4266,7 @@ int launch_render(rtw_gpu_world* g, KArgs& A, int kind, hipStream_t stream) {
     // the allocation holds the kernel's entries, and 16-bit entries hold every node and leaf index
     if ((size_t)stk_entry * g->depth * RTW_BLOCK != stk_bytes || (stk_entry == 2 && !small))
         return rtw::fail(RTW_ERR_UNSUPPORTED, "traversal stack entry width does not match the LDS allocation");
-    const char* ncs = std::getenv("RTW_NO_COOP_SHARE");
-    if (!stats && mode >= 1 && sah && lk == LK_TRIS && A.coop_max > 0 && g->depth >= 1 &&
-        lds + RTW_MB_WORDS * sizeof(uint32_t) <= cap && !(ncs && ncs[0] && ncs[0] != '0')) {
+    if (mb_want && lds + RTW_MB_WORDS * sizeof(uint32_t) <= cap) {
         A.mb_off = A.stack_off + (int32_t)(stk_bytes / sizeof(float4));
         A.mb_cap = std::min(64, g->depth * stk_entry);
         if (const char* e = std::getenv("RTW_MB_CAP"))  // tests: fewer posts per batch (the rest walk again)
