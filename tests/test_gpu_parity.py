@@ -641,6 +641,45 @@ def test_suzanne_depth_capped_tree_in_lds_mode2(worlds, monkeypatch):
     assert_bit_identical(sah, R.render(big, 1, 8, 50, world, seed=5), "suzanne cap 11 vs reference tree")
 
 
+def _prefix_world(seed: int = 9):
+    """Two meshes then a sphere: the first mesh (an image-textured Lambertian, its leaf_info carries the
+    uv flag) is the triangle prefix, the second (another material) is not (tri_prefix_of stops there)."""
+    rng = np.random.default_rng(seed)
+    wb = R.WorldBuilder()
+    img = (rng.uniform(0, 255, (8, 16, 3))).astype(np.uint8)
+    mat_a = wb.material_lambert(wb.texture_image_rgb8(img))
+    mat_b = wb.material_metal_solid((0.8, 0.7, 0.6), 0.05)
+    mat_g = wb.material_lambert_solid((0.5, 0.5, 0.5))
+    g = wb.new_group()
+
+    def soup(n, lo, hi):
+        c = rng.uniform(lo, hi, (n, 1, 3))
+        v = (c + rng.uniform(-0.3, 0.3, (n, 3, 3))).astype(np.float32)
+        uv = rng.uniform(0.0, 1.0, (n, 6)).astype(np.float32)
+        return np.concatenate([v.reshape(n, 9), np.tile(np.float32([0, 1, 0]), (n, 3)), uv], 1).astype(np.float32)
+
+    g.add(wb.new_mesh(soup(120, (-2.0, 0.2, -1.0), (0.0, 2.0, 1.0)), mat_a))
+    g.add(wb.new_mesh(soup(80, (0.0, 0.2, -1.0), (2.0, 2.0, 1.0)), mat_b))
+    g.add(wb.new_obj_sphere(100.0, mat_g).translate((0.0, -100.0, 0.0)))
+    cam = R.Camera.build().vertical_fov(50.0, 9.0 / 16.0).position((0.0, 1.5, 6.0)).look_at((0, 1, 0), (0, 1, 0)).build()
+    return g.build().finish(wb, R.BackgroundColor.sky(), cam)
+
+
+def test_triangle_prefix_world_bit_exact():
+    """walk_leaf_record / leaf_info_of: the leading mesh's leaf records and leaf_info are made up (its
+    material and uv flag), the second mesh's and the sphere's are read; bit-exact against the oracle."""
+    world = _prefix_world()
+    leaves = [world.raw.leaves[i] for i in range(world.raw.leaf_count)]
+    p = 0
+    while (p < len(leaves) and leaves[p].geom_kind == 3 and leaves[p].flags == 0 and leaves[p].geom_index == p
+           and leaves[p].material == leaves[0].material):
+        p += 1
+    assert 0 < p < len(leaves) - 1, p  # a prefix, then leaves whose records are read
+    size = R.Size2i(64, 36)
+    assert_bit_identical(R.render(size, 1, 8, 50, world, seed=3), O.render(world, R.render_params(size, 8, 50, seed=3)),
+                         "triangle prefix world")
+
+
 def _soup_world(n_tri: int, seed: int = 5):
     """A random triangle soup over a ground sphere (mesh worlds of any size)."""
     rng = np.random.default_rng(seed)
