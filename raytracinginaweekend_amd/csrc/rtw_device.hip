@@ -1351,8 +1351,8 @@ __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit
                                              const TB& S) {  // texture.rs:23-53
     for (int guard = 0; guard < 64; ++guard) {
         // the LDS table (launch_render, when it fits): solid-texture kernels each texture's first record,
-        // the other non-GEN kernels all three records, an image texture's third replaced by its image
-        // record (earth_mapped +3 %, perlin_spheres +5 %); the GEN kernels read HBM / L2 (as an LDS table
+        // the other non-GEN kernels all three records (earth_mapped +3 %, perlin_spheres +5 %); the GEN
+        // kernels read HBM / L2 (as an LDS table
         // it cost C5 1.3 % in spills, profiles/r05/ab_tex_lds.txt)
         constexpr bool FULL = TX != TX_SOLID && !TB::gen;
         // GEN kernels with any texture kind get no table from launch_render: no LDS path compiled (with the
@@ -1362,6 +1362,17 @@ __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit
         const int kind = t0.x;
         if (TX == TX_SOLID || kind == RTW_TEX_SOLID)
             return v3(__int_as_float(t0.y), __int_as_float(t0.z), __int_as_float(t0.w));
+        if (kind == RTW_TEX_IMAGE) {
+            // an image texture's first record is {kind, texel offset, width, height} (rtw_world_upload): the
+            // texel is the second load of the chain, not the fourth (record, third record, image record, texel)
+            uint32_t pu = rtw_f2u32_sat(h.u * (float)t0.z);
+            uint32_t pv = rtw_f2u32_sat(h.v * (float)t0.w);
+            pu = min(pu, (uint32_t)(t0.z - 1));
+            pv = min(pv, (uint32_t)(t0.w - 1));
+            if (STATS) st.c[ST_TEXEL]++;
+            const uint32_t px = w.texels[(size_t)t0.y + (size_t)pv * (size_t)t0.z + pu];
+            return v3(tex255(px & 255u), tex255((px >> 8) & 255u), tex255((px >> 16) & 255u));
+        }
         const int4 t1 = FULL && S.tex0 >= 0 ? lds_i4(S.tex0 + 3 * tex + 1) : w.textures[3 * tex + 1];
         if (kind == RTW_TEX_CHECKER) {
             const float f = __int_as_float(t1.x);
@@ -1370,16 +1381,6 @@ __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit
             continue;
         }
         const int4 t2 = FULL && S.tex0 >= 0 ? lds_i4(S.tex0 + 3 * tex + 2) : w.textures[3 * tex + 2];
-        if (kind == RTW_TEX_IMAGE) {
-            const int4 im = FULL && S.tex0 >= 0 ? t2 : w.images[t2.y];
-            uint32_t pu = rtw_f2u32_sat(h.u * (float)im.y);
-            uint32_t pv = rtw_f2u32_sat(h.v * (float)im.z);
-            pu = min(pu, (uint32_t)(im.y - 1));
-            pv = min(pv, (uint32_t)(im.z - 1));
-            if (STATS) st.c[ST_TEXEL]++;
-            const uint32_t px = w.texels[(size_t)im.x + (size_t)pv * (size_t)im.y + pu];
-            return v3(tex255(px & 255u), tex255((px >> 8) & 255u), tex255((px >> 16) & 255u));
-        }
         const int pi = t2.x;
         const float k = marble_k(w.perlin_ranvec + 768 * pi, w.perlin_perm + 768 * pi, w.perlin_bits[pi], h.pos.x,
                                  h.pos.y, h.pos.z, __int_as_float(t1.w));
@@ -2215,12 +2216,8 @@ __device__ __forceinline__ void render_body(const KArgs& A) {
                 int4* tx = reinterpret_cast<int4*>(smem + A.sh_tex0);
                 if constexpr (TX == TX_SOLID || GEN) {  // (the GEN kernels: -1, no table)
                     for (int i = threadIdx.x; i < A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[3 * i];
-                } else {  // all three records; an image texture's third is its image record
-                    for (int i = threadIdx.x; i < 3 * A.texture_count; i += RTW_BLOCK) {
-                        int4 r = w.textures[i];
-                        if (i % 3 == 2 && w.textures[i - 2].x == RTW_TEX_IMAGE) r = w.images[r.y];
-                        tx[i] = r;
-                    }
+                } else {  // all three records
+                    for (int i = threadIdx.x; i < 3 * A.texture_count; i += RTW_BLOCK) tx[i] = w.textures[i];
                 }
             }
         }
@@ -3754,10 +3751,18 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
         const rtw_material& m = w->materials[i];
         mt[(size_t)i] = make_int4(m.kind, m.texture, (int)fbits(m.fuzz), (int)fbits(m.index_of_refraction));
     }
+    // each image's first texel (the texel array below holds the images in order)
+    std::vector<size_t> texel_off((size_t)std::max(1, w->image_count), 0);
+    for (int i = 1; i < w->image_count; ++i)
+        texel_off[(size_t)i] = texel_off[(size_t)i - 1] + (size_t)w->images[i - 1].width * (size_t)w->images[i - 1].height;
     std::vector<int4> tx((size_t)w->texture_count * 3);
     for (int i = 0; i < w->texture_count; ++i) {
         const rtw_texture& t = w->textures[i];
-        tx[3 * (size_t)i] = make_int4(t.kind, (int)fbits(t.color[0]), (int)fbits(t.color[1]), (int)fbits(t.color[2]));
+        // an image texture's first record: {kind, texel offset, width, height} (texture_sample reads no other)
+        tx[3 * (size_t)i] = t.kind == RTW_TEX_IMAGE
+                                ? make_int4(t.kind, (int)texel_off[(size_t)t.image], w->images[t.image].width,
+                                            w->images[t.image].height)
+                                : make_int4(t.kind, (int)fbits(t.color[0]), (int)fbits(t.color[1]), (int)fbits(t.color[2]));
         tx[3 * (size_t)i + 1] = make_int4((int)fbits(t.inv_frequency), t.even, t.odd, (int)fbits(t.scale));
         tx[3 * (size_t)i + 2] = make_int4(t.perlin, t.image, 0, 0);
     }
