@@ -1346,6 +1346,23 @@ __device__ __forceinline__ float marble_k(const float* ranvec, const uint32_t* p
 
 // TX: the world's textures are all SolidColor (TX_SOLID) or not (TX_ANY: checker, marble, image)
 enum { TX_SOLID = 0, TX_ANY = 1 };
+// ImageTexture::value (texture.rs:40-53): the texel at (u, v) of the image whose texels start at `off`
+template <bool STATS>
+__device__ __forceinline__ V3 image_texel(const DWorld& w, int32_t off, int32_t width, int32_t height, const Hit& h,
+                                          Stats& st) {
+    uint32_t pu = rtw_f2u32_sat(h.u * (float)width);
+    uint32_t pv = rtw_f2u32_sat(h.v * (float)height);
+    pu = min(pu, (uint32_t)(width - 1));
+    pv = min(pv, (uint32_t)(height - 1));
+    if (STATS) st.c[ST_TEXEL]++;
+    const uint32_t px = w.texels[(size_t)off + (size_t)pv * (size_t)width + pu];
+    return v3(tex255(px & 255u), tex255((px >> 8) & 255u), tex255((px >> 16) & 255u));
+}
+// device-only material-record bit (above the RTW_MAT_* kinds): the material's texture is an image, whose
+// {texel offset, width << 16 | height} the record carries in z, w (rtw_world_upload; Lambertian, Isotropic
+// and DiffuseLight, which have no fuzz or index of refraction there) -- shading then reads the texel
+// straight after the material record
+#define RTW_DMAT_IMAGE (1 << 8)
 template <bool STATS, int TX, class TB>
 __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit& h, Stats& st,
                                              const TB& S) {  // texture.rs:23-53
@@ -1362,17 +1379,9 @@ __device__ __forceinline__ V3 texture_sample(const DWorld& w, int tex, const Hit
         const int kind = t0.x;
         if (TX == TX_SOLID || kind == RTW_TEX_SOLID)
             return v3(__int_as_float(t0.y), __int_as_float(t0.z), __int_as_float(t0.w));
-        if (kind == RTW_TEX_IMAGE) {
-            // an image texture's first record is {kind, texel offset, width, height} (rtw_world_upload): the
-            // texel is the second load of the chain, not the fourth (record, third record, image record, texel)
-            uint32_t pu = rtw_f2u32_sat(h.u * (float)t0.z);
-            uint32_t pv = rtw_f2u32_sat(h.v * (float)t0.w);
-            pu = min(pu, (uint32_t)(t0.z - 1));
-            pv = min(pv, (uint32_t)(t0.w - 1));
-            if (STATS) st.c[ST_TEXEL]++;
-            const uint32_t px = w.texels[(size_t)t0.y + (size_t)pv * (size_t)t0.z + pu];
-            return v3(tex255(px & 255u), tex255((px >> 8) & 255u), tex255((px >> 16) & 255u));
-        }
+        // an image texture's first record is {kind, texel offset, width, height} (rtw_world_upload): the
+        // texel is the second load of the chain, not the fourth (record, third record, image record, texel)
+        if (kind == RTW_TEX_IMAGE) return image_texel<STATS>(w, t0.y, t0.z, t0.w, h, st);
         const int4 t1 = FULL && S.tex0 >= 0 ? lds_i4(S.tex0 + 3 * tex + 1) : w.textures[3 * tex + 1];
         if (kind == RTW_TEX_CHECKER) {
             const float f = __int_as_float(t1.x);
@@ -1514,7 +1523,8 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
             done = true;
         } else {
                 const int4 M = S.mat >= 0 ? lds_i4(S.mat + h.material) : w.materials[h.material];
-                const int mkind = M.x;
+                const int mkind = M.x & (RTW_DMAT_IMAGE - 1);
+                const bool direct_image = TX != TX_SOLID && (M.x & RTW_DMAT_IMAGE) != 0;
                 // Material::scatter (material.rs:52-114).  At most one texture lookup per bounce:
                 // the albedo of a scattering material or the emission of a DiffuseLight.
                 bool scatters = true;
@@ -1588,7 +1598,9 @@ __device__ __forceinline__ ShadeOut shade(const DWorld* __restrict__ wp, int32_t
                     }
                 }
                 RTW_PT(4);
-                const V3 tc = (tex >= 0) ? texture_sample<STATS, TX>(w, tex, h, st, S) : v3(0.0f, 0.0f, 0.0f);
+                const V3 tc = tex < 0         ? v3(0.0f, 0.0f, 0.0f)
+                              : direct_image ? image_texel<STATS>(w, M.z, (int32_t)((uint32_t)M.w >> 16), M.w & 0xFFFF, h, st)
+                                             : texture_sample<STATS, TX>(w, tex, h, st, S);
                 const V3 emitted = (mkind == RTW_MAT_DIFFUSE_LIGHT) ? tc : v3(0.0f, 0.0f, 0.0f);
                 const V3 albedo = (mkind == RTW_MAT_DIELECTRIC) ? v3(1.0f, 1.0f, 1.0f) : tc;
                 if (scatters) {
@@ -3746,15 +3758,23 @@ extern "C" RTW_API int rtw_world_upload(const rtw_world* w, int device, rtw_gpu_
     const size_t o_tp = L.push(tp.data(), tp.size() * sizeof(float4));
     const size_t o_ta = L.push(ta.data(), ta.size() * sizeof(float4));
     // materials / textures / images / perlin
-    std::vector<int4> mt((size_t)w->material_count);
-    for (int i = 0; i < w->material_count; ++i) {
-        const rtw_material& m = w->materials[i];
-        mt[(size_t)i] = make_int4(m.kind, m.texture, (int)fbits(m.fuzz), (int)fbits(m.index_of_refraction));
-    }
     // each image's first texel (the texel array below holds the images in order)
     std::vector<size_t> texel_off((size_t)std::max(1, w->image_count), 0);
     for (int i = 1; i < w->image_count; ++i)
         texel_off[(size_t)i] = texel_off[(size_t)i - 1] + (size_t)w->images[i - 1].width * (size_t)w->images[i - 1].height;
+    std::vector<int4> mt((size_t)w->material_count);
+    for (int i = 0; i < w->material_count; ++i) {
+        const rtw_material& m = w->materials[i];
+        mt[(size_t)i] = make_int4(m.kind, m.texture, (int)fbits(m.fuzz), (int)fbits(m.index_of_refraction));
+        // a Lambertian, Isotropic or DiffuseLight over an image texture carries the image (RTW_DMAT_IMAGE)
+        if ((m.kind == RTW_MAT_LAMBERT || m.kind == RTW_MAT_ISOTROPIC || m.kind == RTW_MAT_DIFFUSE_LIGHT) &&
+            w->textures[m.texture].kind == RTW_TEX_IMAGE) {
+            const rtw_image& I = w->images[w->textures[m.texture].image];
+            if (I.width < 65536 && I.height < 65536)
+                mt[(size_t)i] = make_int4(m.kind | RTW_DMAT_IMAGE, m.texture, (int)texel_off[(size_t)w->textures[m.texture].image],
+                                          (int)(((uint32_t)I.width << 16) | (uint32_t)I.height));
+        }
+    }
     std::vector<int4> tx((size_t)w->texture_count * 3);
     for (int i = 0; i < w->texture_count; ++i) {
         const rtw_texture& t = w->textures[i];
