@@ -835,7 +835,7 @@ __device__ __forceinline__ TriFast load_tri(const float4* __restrict__ tf, int i
 // 2).  The stride: RTW_TRI_SOA records, a compile-time constant whose four reads share one address register
 // (offsets 0, 16, 32, 48 KB in the ds_read_b128 immediate) -- except in the triangle-and-sphere kernels
 // (LK_TRIS), whose stride is the world's triangle count (KArgs::tri_stride): three adds per test, and the
-// 3.5 KB that let suzanne's split tree take mode 2 (DESIGN 5.3).  (The runtime stride in every kernel cost
+// 3.5 KB that let suzanne's split tree take mode 2 (DESIGN 4).  (The runtime stride in every kernel cost
 // cornell_cube 2 %, profiles/r06/ab_mode2_suzanne.txt.)
 #ifndef RTW_TRI_SOA
 #define RTW_TRI_SOA 1024
@@ -3389,7 +3389,7 @@ SahTables build_sah_tables(const rtw_world* w) {
         // LDS) is rebuilt with the largest depth cap that lets it in, down to ceil(log2 L) + 5 levels (worlds
         // of plain triangles and spheres: the LK_TRIS kernels' layout, lds_mode2_bytes).
         // suzanne: depth 21 -> 16, 1770 -> 1719 nodes, node tests per ray +0.5 %, leaf tests +1.7 %
-        // (tools/sah_cost.py), and the triangle records in LDS: DESIGN 5.3.
+        // (tools/sah_cost.py), and the triangle records in LDS: DESIGN 4.
         bool tris_spheres = true;  // the kernels with the exact triangle stride and the prefix (LK_TRIS)
         for (int32_t i = 0; i < L; ++i)
             if ((w->leaves[i].geom_kind != RTW_GEOM_TRIANGLE && w->leaves[i].geom_kind != RTW_GEOM_SPHERE) ||
