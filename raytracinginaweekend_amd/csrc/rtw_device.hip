@@ -3405,8 +3405,13 @@ SahTables build_sah_tables(const rtw_world* w) {
             };
             int lb = 5;
             while ((1 << (lb - 5)) < L) ++lb;
+            // the first cap tried: two levels above the deepest stack that fits with the uncapped tree's node
+            // count (a capped tree has a few nodes fewer: suzanne 17, then 16 -- two builds of ~0.3 s, not five)
+            int first = sdepth - 1;
+            for (int d = lb; d < sdepth; ++d)
+                if (fits2(split.size(), d)) first = std::min(sdepth - 1, d + 2);
             if (!fits2(split.size(), sdepth) && fits2((size_t)L - 1, lb))
-                for (int c = sdepth - 1; c >= lb; --c) {
+                for (int c = first; c >= lb; --c) {
                     std::vector<rtw_bvh_node> s2;
                     std::vector<float> k2v;
                     int32_t r2 = 0;
